@@ -1,0 +1,36 @@
+# Build of every native artefact (hipcc cross-compiles gfx950 without a GPU).
+#   make            -> library + drivers + oracle
+#   make lib        -> spmm_amd/lib/libmi355_spgemm.so  (the product)
+#   make drivers    -> drivers/bin/spgemm_from_txt_alg{1,2,3}
+#   make oracle     -> oracle/liboracle.so              (test infrastructure)
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -Wall
+LIB      := spmm_amd/lib/libmi355_spgemm.so
+SRC      := spmm_amd/csrc/spgemm.hip
+HDRS     := include/spgemm.h spmm_amd/csrc/spg_device.hpp spmm_amd/csrc/spgemm_kernels.hpp
+DRIVERS  := drivers/bin/spgemm_from_txt_alg1 drivers/bin/spgemm_from_txt_alg2 drivers/bin/spgemm_from_txt_alg3
+
+all: lib drivers oracle
+lib: $(LIB)
+drivers: $(DRIVERS)
+
+$(LIB): $(SRC) $(HDRS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -shared -Iinclude -Ispmm_amd/csrc $(SRC) -o $@
+
+# the three reference driver names, one source; ALG fixed at compile time
+drivers/bin/spgemm_from_txt_alg%: drivers/spgemm_from_txt.cpp include/spgemm.h $(LIB)
+	@mkdir -p $(dir $@)
+	g++ -O2 -std=c++17 -Wall -DSPG_DRIVER_ALG=$* -Iinclude -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ \
+	    $< -o $@ -L$(abspath spmm_amd/lib) -lmi355_spgemm -L/opt/rocm/lib -lamdhip64 \
+	    -Wl,-rpath,'$$ORIGIN/../../spmm_amd/lib' -Wl,-rpath,/opt/rocm/lib
+
+oracle:
+	$(MAKE) -s -C oracle liboracle.so
+
+clean:
+	rm -f $(LIB) $(DRIVERS)
+	$(MAKE) -s -C oracle clean
+
+.PHONY: all lib drivers oracle clean

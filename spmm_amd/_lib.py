@@ -1,0 +1,143 @@
+"""ctypes binding of libmi355_spgemm.so (include/spgemm.h).
+
+Plays the role of the reference's Cython layer
+(modify_src/cupy-src/cupy_backends/cuda/libs/cusparse.pyx:5063-5152, status handling
+:1526-1547): thin wrappers that turn a non-zero status into an exception.
+
+The library is loaded after ``torch`` so that it binds to the HIP runtime torch already
+loaded (same SONAME, libamdhip64.so.7) and device pointers from torch's allocator are
+valid in it.  There is no CPU fallback: if the library is missing the import of the
+product path fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must be loaded before the HIP library, see module doc)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libmi355_spgemm.so")
+
+# enums of include/spgemm.h
+SPG_INDEX_32I = 32
+SPG_INDEX_64I = 64
+SPG_R_32F = 0
+SPG_R_64F = 1
+SPG_ALG_DEFAULT, SPG_ALG1, SPG_ALG2, SPG_ALG3 = 0, 1, 2, 3
+
+STATUS_NAMES = {
+    0: "SPG_STATUS_SUCCESS", 1: "SPG_STATUS_NOT_INITIALIZED", 2: "SPG_STATUS_ALLOC_FAILED",
+    3: "SPG_STATUS_INVALID_VALUE", 4: "SPG_STATUS_ARCH_MISMATCH",
+    6: "SPG_STATUS_EXECUTION_FAILED", 7: "SPG_STATUS_INTERNAL_ERROR",
+    10: "SPG_STATUS_NOT_SUPPORTED", 11: "SPG_STATUS_INSUFFICIENT_RESOURCES",
+    100: "SPG_STATUS_OVERFLOW", 101: "SPG_STATUS_HIP_ERROR",
+}
+STATUS_ALLOC_FAILED = 2
+STATUS_OVERFLOW = 100
+
+# every symbol include/spgemm.h declares (tests/test_abi.py checks the .so exports them)
+EXPORTS = ("spg_version", "spg_status_string", "spg_create", "spg_destroy", "spg_set_stream",
+           "spg_last_hip_error", "spg_plan", "spg_num_products", "spg_symbolic",
+           "spg_numeric", "spg_peak_bytes", "spg_validate_csr", "spg_plan_destroy")
+
+
+class SpgCsr(ctypes.Structure):
+    """spg_csr_t"""
+    _fields_ = [("rows", ctypes.c_int64), ("cols", ctypes.c_int64), ("nnz", ctypes.c_int64),
+                ("indptr", ctypes.c_void_p), ("indices", ctypes.c_void_p),
+                ("values", ctypes.c_void_p), ("indptr_type", ctypes.c_int),
+                ("value_type", ctypes.c_int)]
+
+
+class SpgError(RuntimeError):
+    """Non-zero spg_status_t (the analogue of CuPy's CuSparseError)."""
+
+    def __init__(self, status: int, where: str = ""):
+        self.status = int(status)
+        name = STATUS_NAMES.get(self.status, f"SPG_STATUS_{self.status}")
+        super().__init__(f"{where}: {name}" if where else name)
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load():
+    """Load and prototype the library once.  Raises RuntimeError if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"{LIB_PATH} is missing: build it with `python -c \"import __graft_entry__ as g; "
+                f"g.build()\"` (hipcc --offload-arch=gfx950)")
+        lib = ctypes.CDLL(LIB_PATH)
+        vp, i64, sz = ctypes.c_void_p, ctypes.c_int64, ctypes.c_size_t
+        csrp = ctypes.POINTER(SpgCsr)
+        proto = {
+            "spg_version": (ctypes.c_int, []),
+            "spg_status_string": (ctypes.c_char_p, [ctypes.c_int]),
+            "spg_create": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.c_int]),
+            "spg_destroy": (ctypes.c_int, [vp]),
+            "spg_set_stream": (ctypes.c_int, [vp, vp]),
+            "spg_last_hip_error": (ctypes.c_int, [vp]),
+            "spg_plan": (ctypes.c_int, [vp, csrp, csrp, ctypes.c_int, ctypes.c_float,
+                                        ctypes.POINTER(sz), vp, ctypes.POINTER(vp)]),
+            "spg_num_products": (ctypes.c_int, [vp, vp, ctypes.POINTER(i64)]),
+            "spg_symbolic": (ctypes.c_int, [vp, vp, vp, ctypes.c_int, ctypes.POINTER(i64)]),
+            "spg_numeric": (ctypes.c_int, [vp, vp, vp, csrp]),
+            "spg_peak_bytes": (ctypes.c_int, [vp, ctypes.POINTER(sz)]),
+            "spg_validate_csr": (ctypes.c_int, [vp, csrp, ctypes.POINTER(ctypes.c_int)]),
+            "spg_plan_destroy": (ctypes.c_int, [vp]),
+        }
+        for name, (res, args) in proto.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def check(status: int, where: str = "") -> None:
+    if status != 0:
+        raise SpgError(status, where)
+
+
+class Handle:
+    """spg_handle_t bound to one device (one per host thread per device, like CuPy's
+    thread-local cuSPARSE handles, cupy-src/cupy/cuda/device.pyx:228-243)."""
+
+    def __init__(self, device: int):
+        self.lib = load()
+        self.device = device
+        h = ctypes.c_void_p()
+        check(self.lib.spg_create(ctypes.byref(h), device), "spg_create")
+        self.ptr = h
+
+    def set_stream(self, stream_ptr: int) -> None:
+        check(self.lib.spg_set_stream(self.ptr, ctypes.c_void_p(stream_ptr)), "spg_set_stream")
+
+    def __del__(self):
+        try:
+            if getattr(self, "ptr", None):
+                self.lib.spg_destroy(self.ptr)
+        except Exception:
+            pass
+
+
+_tls = threading.local()
+
+
+def get_handle(device: int) -> Handle:
+    hs = getattr(_tls, "handles", None)
+    if hs is None:
+        hs = _tls.handles = {}
+    h = hs.get(device)
+    if h is None:
+        h = hs[device] = Handle(device)
+    return h

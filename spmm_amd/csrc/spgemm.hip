@@ -1,0 +1,595 @@
+// spgemm.hip -- libmi355_spgemm.so: the C ABI declared in include/spgemm.h.
+//
+// Host side of the engine: argument checking, workspace carving, algorithm sequencing
+// (ALG1 single pass, ALG2 two phase, ALG3 chunked two phase) and type dispatch to the
+// kernels in spgemm_kernels.hpp.  No HIP or C++ type crosses the ABI.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "spgemm.h"
+#include "spgemm_kernels.hpp"
+
+using namespace spg;
+
+struct spg_handle_s {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int last_hip = 0;
+    int64_t* pinned = nullptr;      // 8 host-pinned int64 for device->host scalars
+    void* scratch = nullptr;        // internal device scratch (plan-time analysis)
+    size_t scratch_bytes = 0;
+    // per-phase timing (spg_set_timing / spg_get_timing)
+    bool timing = false;
+    struct Pending { int phase; hipEvent_t a, b; };
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> pool;
+    double ms[SPG_NUM_PHASES] = {};
+    int64_t launches[SPG_NUM_PHASES] = {};
+};
+
+struct spg_plan_s {
+    spg_csr_t A{}, B{};
+    spg_alg_t alg = SPG_ALG2;
+    float cf = 0.2f;
+    char* ws = nullptr;
+    size_t ws_bytes = 0;
+    // workspace carve
+    int64_t* scalars = nullptr;     // [0] total, [1] overflow, [2..] flags
+    int64_t* row_cnt = nullptr;     // rows
+    uint32_t* seg = nullptr;        // 2 * seg_len
+    int64_t seg_len = 0;
+    int64_t* ub = nullptr;          // ALG1: product prefix, rows + 1
+    int32_t* tj = nullptr;          // ALG1: upper-bound column buffer (P entries)
+    void* tx = nullptr;             // ALG1: upper-bound value buffer (P entries)
+    int64_t P = -1;                 // number of products, -1 until known
+    int64_t nnzC = -1;
+    void* c_indptr = nullptr;
+    spg_index_t c_indptr_type = SPG_INDEX_32I;
+    std::vector<int64_t> chunk_rows;   // ALG3 row boundaries (chunk c = [r[c], r[c+1]))
+    std::vector<int64_t> chunk_nz;     // A entry offset of each boundary
+};
+
+// ----------------------------------------------------------------------------- helpers
+namespace {
+
+inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
+
+inline size_t vbytes(spg_dtype_t t) { return t == SPG_R_64F ? 8 : 4; }
+
+inline int64_t grid_for(int64_t rows, int per_block) { return (rows + per_block - 1) / per_block; }
+
+spg_status_t hip_fail(spg_handle_t h, hipError_t e) {
+    if (h) h->last_hip = (int)e;
+    if (e == hipErrorOutOfMemory) return SPG_STATUS_ALLOC_FAILED;
+    return SPG_STATUS_HIP_ERROR;
+}
+
+#define SPG_HIP(h, expr)                                  \
+    do {                                                  \
+        hipError_t e_ = (expr);                           \
+        if (e_ != hipSuccess) return hip_fail((h), e_);   \
+    } while (0)
+
+#define SPG_LAUNCHED(h) SPG_HIP(h, hipGetLastError())
+
+hipEvent_t take_event(spg_handle_t h) {
+    if (!h->pool.empty()) {
+        hipEvent_t e = h->pool.back();
+        h->pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+// Brackets the kernel launches of one phase with events when timing is enabled.
+struct PhaseTimer {
+    spg_handle_t h;
+    int phase;
+    hipEvent_t a = nullptr;
+    PhaseTimer(spg_handle_t h_, int phase_) : h(h_), phase(phase_) {
+        if (h->timing && (a = take_event(h))) (void)hipEventRecord(a, h->stream);
+    }
+    ~PhaseTimer() {
+        if (!a) return;
+        hipEvent_t b = take_event(h);
+        if (!b) { h->pool.push_back(a); return; }
+        (void)hipEventRecord(b, h->stream);
+        h->pending.push_back({phase, a, b});
+    }
+};
+
+spg_status_t check_csr(const spg_csr_t* M) {
+    if (!M) return SPG_STATUS_INVALID_VALUE;
+    if (M->rows < 0 || M->cols < 0 || M->nnz < 0) return SPG_STATUS_INVALID_VALUE;
+    if (M->cols > 2147483647LL) return SPG_STATUS_NOT_SUPPORTED;   // int32 column indices
+    if (M->indptr_type != SPG_INDEX_32I && M->indptr_type != SPG_INDEX_64I)
+        return SPG_STATUS_INVALID_VALUE;
+    if (M->value_type != SPG_R_32F && M->value_type != SPG_R_64F) return SPG_STATUS_NOT_SUPPORTED;
+    if (M->indptr_type == SPG_INDEX_32I && M->nnz > 2147483647LL) return SPG_STATUS_INVALID_VALUE;
+    if (!M->indptr && M->rows >= 0) return SPG_STATUS_INVALID_VALUE;
+    if (M->nnz > 0 && (!M->indices || !M->values)) return SPG_STATUS_INVALID_VALUE;
+    return SPG_STATUS_SUCCESS;
+}
+
+spg_status_t ensure_scratch(spg_handle_t h, size_t bytes) {
+    if (h->scratch_bytes >= bytes) return SPG_STATUS_SUCCESS;
+    if (h->scratch) {
+        SPG_HIP(h, hipStreamSynchronize(h->stream));
+        SPG_HIP(h, hipFree(h->scratch));
+        h->scratch = nullptr;
+        h->scratch_bytes = 0;
+    }
+    SPG_HIP(h, hipMalloc(&h->scratch, bytes));
+    h->scratch_bytes = bytes;
+    return SPG_STATUS_SUCCESS;
+}
+
+// Product prefix of every row into `pref` (rows + 1 int64) and its total into scal[0].
+template <typename IP>
+spg_status_t launch_products(spg_handle_t h, const spg_csr_t& A, const spg_csr_t& B,
+                             int64_t* cnt, int64_t* pref, int64_t* scal) {
+    const int64_t rows = A.rows;
+    if (rows > 0) {
+        PhaseTimer pt(h, SPG_PHASE_PRODUCTS);
+        hipLaunchKernelGGL(k_row_products<IP>, dim3((unsigned)grid_for(rows, WPB)), dim3(BLOCK), 0,
+                           h->stream, rows, (const IP*)A.indptr, (const int32_t*)A.indices,
+                           (const IP*)B.indptr, cnt);
+        SPG_LAUNCHED(h);
+    }
+    PhaseTimer pt(h, SPG_PHASE_SCAN);
+    hipLaunchKernelGGL(k_scan_excl<int64_t>, dim3(1), dim3(1024), 0, h->stream, rows,
+                       (const int64_t*)cnt, pref, scal);
+    SPG_LAUNCHED(h);
+    return SPG_STATUS_SUCCESS;
+}
+
+spg_status_t products_prefix(spg_handle_t h, const spg_csr_t& A, const spg_csr_t& B,
+                             int64_t* cnt, int64_t* pref, int64_t* scal) {
+    return A.indptr_type == SPG_INDEX_64I ? launch_products<int64_t>(h, A, B, cnt, pref, scal)
+                                          : launch_products<int32_t>(h, A, B, cnt, pref, scal);
+}
+
+spg_status_t read_scalars(spg_handle_t h, const int64_t* dev, int n, int64_t* out) {
+    SPG_HIP(h, hipMemcpyAsync(h->pinned, dev, sizeof(int64_t) * n, hipMemcpyDeviceToHost, h->stream));
+    SPG_HIP(h, hipStreamSynchronize(h->stream));
+    for (int i = 0; i < n; ++i) out[i] = h->pinned[i];
+    return SPG_STATUS_SUCCESS;
+}
+
+struct Layout {
+    size_t scalars = 0, row_cnt = 0, seg = 0, ub = 0, tj = 0, tx = 0, total = 0;
+};
+
+Layout make_layout(const spg_plan_s& p) {
+    Layout L;
+    size_t off = 0;
+    L.scalars = off; off = align_up(off + 16 * sizeof(int64_t));
+    L.row_cnt = off; off = align_up(off + sizeof(int64_t) * (size_t)(p.A.rows + 1));
+    L.seg = off;     off = align_up(off + sizeof(uint32_t) * 2 * (size_t)std::max<int64_t>(p.seg_len, 1));
+    if (p.alg == SPG_ALG1) {
+        L.ub = off; off = align_up(off + sizeof(int64_t) * (size_t)(p.A.rows + 1));
+        L.tj = off; off = align_up(off + sizeof(int32_t) * (size_t)std::max<int64_t>(p.P, 1));
+        L.tx = off; off = align_up(off + vbytes(p.A.value_type) * (size_t)std::max<int64_t>(p.P, 1));
+    }
+    L.total = off;
+    return L;
+}
+
+void carve(spg_plan_s& p, const Layout& L) {
+    p.scalars = (int64_t*)(p.ws + L.scalars);
+    p.row_cnt = (int64_t*)(p.ws + L.row_cnt);
+    p.seg = (uint32_t*)(p.ws + L.seg);
+    if (p.alg == SPG_ALG1) {
+        p.ub = (int64_t*)(p.ws + L.ub);
+        p.tj = (int32_t*)(p.ws + L.tj);
+        p.tx = (void*)(p.ws + L.tx);
+    }
+}
+
+// ALG3: cut rows into chunks of at most max(cf * P, largest row) products.
+spg_status_t plan_chunks(spg_handle_t h, spg_plan_s& p) {
+    const int64_t rows = p.A.rows;
+    p.chunk_rows.assign({0, rows});
+    p.chunk_nz.assign({0, p.A.nnz});
+    p.seg_len = p.A.nnz;
+    if (rows == 0) return SPG_STATUS_SUCCESS;
+    spg_status_t st = ensure_scratch(h, sizeof(int64_t) * (2 * (size_t)rows + 18));
+    if (st) return st;
+    int64_t* cnt = (int64_t*)h->scratch;
+    int64_t* pref = cnt + rows;
+    int64_t* scal = pref + rows + 1;
+    if ((st = products_prefix(h, p.A, p.B, cnt, pref, scal))) return st;
+    std::vector<int64_t> hp((size_t)rows + 1), ha((size_t)rows + 1);
+    SPG_HIP(h, hipMemcpyAsync(hp.data(), pref, sizeof(int64_t) * (rows + 1), hipMemcpyDeviceToHost, h->stream));
+    if (p.A.indptr_type == SPG_INDEX_64I) {
+        SPG_HIP(h, hipMemcpyAsync(ha.data(), p.A.indptr, sizeof(int64_t) * (rows + 1),
+                                  hipMemcpyDeviceToHost, h->stream));
+        SPG_HIP(h, hipStreamSynchronize(h->stream));
+    } else {
+        std::vector<int32_t> t((size_t)rows + 1);
+        SPG_HIP(h, hipMemcpyAsync(t.data(), p.A.indptr, sizeof(int32_t) * (rows + 1),
+                                  hipMemcpyDeviceToHost, h->stream));
+        SPG_HIP(h, hipStreamSynchronize(h->stream));
+        for (int64_t i = 0; i <= rows; ++i) ha[(size_t)i] = t[(size_t)i];
+    }
+    p.P = hp[(size_t)rows];
+    const int64_t cap = std::max<int64_t>(1, (int64_t)std::ceil((double)p.cf * (double)p.P));
+    p.chunk_rows.assign(1, 0);
+    p.chunk_nz.assign(1, ha[0]);
+    int64_t r = 0;
+    while (r < rows) {
+        // furthest row end e with pref[e] - pref[r] <= cap (at least one row)
+        const int64_t target = hp[(size_t)r] + cap;
+        int64_t e = (int64_t)(std::upper_bound(hp.begin() + r + 1, hp.end(), target) - hp.begin()) - 1;
+        if (e <= r) e = r + 1;
+        p.chunk_rows.push_back(e);
+        p.chunk_nz.push_back(ha[(size_t)e]);
+        r = e;
+    }
+    int64_t mx = 0;
+    for (size_t c = 0; c + 1 < p.chunk_nz.size(); ++c)
+        mx = std::max(mx, p.chunk_nz[c + 1] - p.chunk_nz[c]);
+    p.seg_len = mx;
+    return SPG_STATUS_SUCCESS;
+}
+
+// --------------------------------------------------------------------- typed launchers
+template <typename IP>
+spg_status_t run_symbolic_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_t r1, int64_t nz0) {
+    const int64_t n = r1 - r0;
+    if (n <= 0) return SPG_STATUS_SUCCESS;
+    PhaseTimer pt(h, SPG_PHASE_SYMBOLIC);
+    hipLaunchKernelGGL(k_symbolic<IP>, dim3((unsigned)grid_for(n, WPB)), dim3(BLOCK), 0, h->stream,
+                       r0, n, p.B.cols, (const IP*)p.A.indptr, (const int32_t*)p.A.indices,
+                       (const IP*)p.B.indptr, (const int32_t*)p.B.indices, p.row_cnt, p.seg, nz0);
+    SPG_LAUNCHED(h);
+    return SPG_STATUS_SUCCESS;
+}
+
+template <typename T, typename IP, typename OFF, bool UB>
+spg_status_t run_numeric_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_t r1, int64_t nz0,
+                              const OFF* off, int32_t* cj, T* cx, T alpha) {
+    const int64_t n = r1 - r0;
+    if (n <= 0) return SPG_STATUS_SUCCESS;
+    PhaseTimer pt(h, SPG_PHASE_NUMERIC);
+    hipLaunchKernelGGL((k_numeric<T, IP, OFF, UB>), dim3((unsigned)grid_for(n, WPB)), dim3(BLOCK), 0,
+                       h->stream, r0, n, p.B.cols, (const IP*)p.A.indptr,
+                       (const int32_t*)p.A.indices, (const T*)p.A.values, (const IP*)p.B.indptr,
+                       (const int32_t*)p.B.indices, (const T*)p.B.values, off, cj, cx, alpha,
+                       p.row_cnt, p.seg, nz0, p.seg_len);
+    SPG_LAUNCHED(h);
+    return SPG_STATUS_SUCCESS;
+}
+
+template <typename OUT>
+spg_status_t run_scan(spg_handle_t h, spg_plan_s& p, void* out) {
+    PhaseTimer pt(h, SPG_PHASE_SCAN);
+    hipLaunchKernelGGL(k_scan_excl<OUT>, dim3(1), dim3(1024), 0, h->stream, p.A.rows,
+                       (const int64_t*)p.row_cnt, (OUT*)out, p.scalars);
+    SPG_LAUNCHED(h);
+    return SPG_STATUS_SUCCESS;
+}
+
+template <typename IP>
+spg_status_t symbolic_typed(spg_handle_t h, spg_plan_s& p) {
+    spg_status_t st;
+    if (p.alg == SPG_ALG3) {
+        for (size_t c = 0; c + 1 < p.chunk_rows.size(); ++c)
+            if ((st = run_symbolic_rows<IP>(h, p, p.chunk_rows[c], p.chunk_rows[c + 1], p.chunk_nz[c])))
+                return st;
+        return SPG_STATUS_SUCCESS;
+    }
+    int64_t nz0 = 0;
+    return run_symbolic_rows<IP>(h, p, 0, p.A.rows, nz0);
+}
+
+template <typename T, typename IP>
+spg_status_t alg1_compute(spg_handle_t h, spg_plan_s& p) {
+    // upper-bound offsets = product prefix, then the fused structure+value pass
+    spg_status_t st = products_prefix(h, p.A, p.B, p.row_cnt, p.ub, p.scalars);
+    if (st) return st;
+    return run_numeric_rows<T, IP, int64_t, true>(h, p, 0, p.A.rows, 0, p.ub, p.tj, (T*)p.tx, (T)1);
+}
+
+template <typename T, typename IP, typename IPC>
+spg_status_t numeric_typed(spg_handle_t h, spg_plan_s& p, const spg_csr_t& C, T alpha) {
+    const IPC* cp = (const IPC*)C.indptr;
+    if (p.alg == SPG_ALG1) {
+        if (p.A.rows > 0) {
+            PhaseTimer pt(h, SPG_PHASE_COMPACT);
+            hipLaunchKernelGGL((k_compact<T, IPC>), dim3((unsigned)grid_for(p.A.rows, WPB)), dim3(BLOCK), 0,
+                               h->stream, p.A.rows, (const int64_t*)p.ub, cp, (const int32_t*)p.tj,
+                               (const T*)p.tx, (int32_t*)C.indices, (T*)C.values, alpha);
+            SPG_LAUNCHED(h);
+        }
+        return SPG_STATUS_SUCCESS;
+    }
+    spg_status_t st;
+    if (p.alg == SPG_ALG3) {
+        for (size_t c = 0; c + 1 < p.chunk_rows.size(); ++c)
+            if ((st = run_numeric_rows<T, IP, IPC, false>(h, p, p.chunk_rows[c], p.chunk_rows[c + 1],
+                                                          p.chunk_nz[c], cp, (int32_t*)C.indices,
+                                                          (T*)C.values, alpha)))
+                return st;
+        return SPG_STATUS_SUCCESS;
+    }
+    return run_numeric_rows<T, IP, IPC, false>(h, p, 0, p.A.rows, 0, cp, (int32_t*)C.indices,
+                                               (T*)C.values, alpha);
+}
+
+template <typename IP>
+spg_status_t validate_typed(spg_handle_t h, const spg_csr_t& M, int* flags) {
+    if (M.rows > 0) {
+        PhaseTimer pt(h, SPG_PHASE_VALIDATE);
+        hipLaunchKernelGGL(k_validate<IP>, dim3((unsigned)grid_for(M.rows, BLOCK)), dim3(BLOCK), 0,
+                           h->stream, M.rows, M.cols, M.nnz, (const IP*)M.indptr,
+                           (const int32_t*)M.indices, flags);
+        SPG_LAUNCHED(h);
+    }
+    return SPG_STATUS_SUCCESS;
+}
+
+}  // namespace
+
+// =============================================================================== C ABI
+extern "C" {
+
+int spg_version(void) { return SPG_VERSION_MAJOR * 10000 + SPG_VERSION_MINOR * 100 + SPG_VERSION_PATCH; }
+
+const char* spg_status_string(spg_status_t s) {
+    switch (s) {
+        case SPG_STATUS_SUCCESS: return "SPG_STATUS_SUCCESS";
+        case SPG_STATUS_NOT_INITIALIZED: return "SPG_STATUS_NOT_INITIALIZED";
+        case SPG_STATUS_ALLOC_FAILED: return "SPG_STATUS_ALLOC_FAILED";
+        case SPG_STATUS_INVALID_VALUE: return "SPG_STATUS_INVALID_VALUE";
+        case SPG_STATUS_ARCH_MISMATCH: return "SPG_STATUS_ARCH_MISMATCH";
+        case SPG_STATUS_EXECUTION_FAILED: return "SPG_STATUS_EXECUTION_FAILED";
+        case SPG_STATUS_INTERNAL_ERROR: return "SPG_STATUS_INTERNAL_ERROR";
+        case SPG_STATUS_NOT_SUPPORTED: return "SPG_STATUS_NOT_SUPPORTED";
+        case SPG_STATUS_INSUFFICIENT_RESOURCES: return "SPG_STATUS_INSUFFICIENT_RESOURCES";
+        case SPG_STATUS_OVERFLOW: return "SPG_STATUS_OVERFLOW";
+        case SPG_STATUS_HIP_ERROR: return "SPG_STATUS_HIP_ERROR";
+    }
+    return "SPG_STATUS_UNKNOWN";
+}
+
+spg_status_t spg_create(spg_handle_t* handle, int hip_device) {
+    if (!handle) return SPG_STATUS_INVALID_VALUE;
+    *handle = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return SPG_STATUS_NOT_INITIALIZED;
+    int dev = hip_device;
+    if (dev < 0) {
+        if (hipGetDevice(&dev) != hipSuccess) return SPG_STATUS_NOT_INITIALIZED;
+    }
+    if (dev >= ndev) return SPG_STATUS_INVALID_VALUE;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return SPG_STATUS_NOT_INITIALIZED;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return SPG_STATUS_ARCH_MISMATCH;
+    spg_handle_s* h = new (std::nothrow) spg_handle_s();
+    if (!h) return SPG_STATUS_ALLOC_FAILED;
+    h->device = dev;
+    hipError_t e = hipSetDevice(dev);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&h->pinned, 16 * sizeof(int64_t), hipHostMallocDefault);
+    if (e != hipSuccess) {
+        delete h;
+        return e == hipErrorOutOfMemory ? SPG_STATUS_ALLOC_FAILED : SPG_STATUS_HIP_ERROR;
+    }
+    *handle = h;
+    return SPG_STATUS_SUCCESS;
+}
+
+spg_status_t spg_destroy(spg_handle_t h) {
+    if (!h) return SPG_STATUS_NOT_INITIALIZED;
+    if (h->scratch) {
+        (void)hipStreamSynchronize(h->stream);
+        (void)hipFree(h->scratch);
+    }
+    if (h->pinned) (void)hipHostFree(h->pinned);
+    for (auto& q : h->pending) { (void)hipEventDestroy(q.a); (void)hipEventDestroy(q.b); }
+    for (hipEvent_t e : h->pool) (void)hipEventDestroy(e);
+    delete h;
+    return SPG_STATUS_SUCCESS;
+}
+
+spg_status_t spg_set_stream(spg_handle_t h, void* stream) {
+    if (!h) return SPG_STATUS_NOT_INITIALIZED;
+    h->stream = (hipStream_t)stream;
+    return SPG_STATUS_SUCCESS;
+}
+
+int spg_last_hip_error(spg_handle_t h) { return h ? h->last_hip : 0; }
+
+spg_status_t spg_plan(spg_handle_t h, const spg_csr_t* A, const spg_csr_t* B, spg_alg_t alg,
+                      float chunk_fraction, size_t* workspace_bytes, void* workspace,
+                      spg_plan_t* plan) {
+    if (!h) return SPG_STATUS_NOT_INITIALIZED;
+    if (!workspace_bytes) return SPG_STATUS_INVALID_VALUE;
+    spg_status_t st;
+    if ((st = check_csr(A)) || (st = check_csr(B))) return st;
+    if (A->cols != B->rows) return SPG_STATUS_INVALID_VALUE;
+    if (A->value_type != B->value_type) return SPG_STATUS_INVALID_VALUE;
+    if (A->indptr_type != B->indptr_type) return SPG_STATUS_INVALID_VALUE;
+    if (alg != SPG_ALG_DEFAULT && alg != SPG_ALG1 && alg != SPG_ALG2 && alg != SPG_ALG3)
+        return SPG_STATUS_INVALID_VALUE;
+    if (alg == SPG_ALG3 && !(chunk_fraction > 0.0f && chunk_fraction <= 1.0f))
+        return SPG_STATUS_INVALID_VALUE;
+    if (workspace && !plan) return SPG_STATUS_INVALID_VALUE;
+    SPG_HIP(h, hipSetDevice(h->device));
+
+    spg_plan_s tmp;
+    tmp.A = *A;
+    tmp.B = *B;
+    tmp.alg = alg == SPG_ALG_DEFAULT ? SPG_ALG2 : alg;
+    tmp.cf = chunk_fraction;
+    tmp.seg_len = A->nnz;
+    if (tmp.alg == SPG_ALG1) {
+        // size the upper-bound buffers from the exact product count (waits for the device)
+        if ((st = ensure_scratch(h, sizeof(int64_t) * (2 * (size_t)A->rows + 18)))) return st;
+        int64_t* cnt = (int64_t*)h->scratch;
+        int64_t* pref = cnt + A->rows;
+        int64_t* scal = pref + A->rows + 1;
+        if ((st = products_prefix(h, *A, *B, cnt, pref, scal))) return st;
+        if ((st = read_scalars(h, scal, 1, &tmp.P))) return st;
+    } else if (tmp.alg == SPG_ALG3) {
+        if ((st = plan_chunks(h, tmp))) return st;
+    }
+    const Layout L = make_layout(tmp);
+    if (!workspace) {
+        *workspace_bytes = L.total;
+        return SPG_STATUS_SUCCESS;
+    }
+    if (*workspace_bytes < L.total) return SPG_STATUS_INVALID_VALUE;
+    spg_plan_s* p = new (std::nothrow) spg_plan_s(std::move(tmp));
+    if (!p) return SPG_STATUS_ALLOC_FAILED;
+    p->ws = (char*)workspace;
+    p->ws_bytes = *workspace_bytes;
+    carve(*p, L);
+    *plan = p;
+    return SPG_STATUS_SUCCESS;
+}
+
+spg_status_t spg_num_products(spg_handle_t h, spg_plan_t p, int64_t* num_products) {
+    if (!h) return SPG_STATUS_NOT_INITIALIZED;
+    if (!p || !num_products) return SPG_STATUS_INVALID_VALUE;
+    if (p->P < 0) {
+        SPG_HIP(h, hipSetDevice(h->device));
+        spg_status_t st;
+        // row_cnt doubles as the per-row count buffer; scalars[2] receives the total
+        int64_t* pref = (int64_t*)h->scratch;
+        if ((st = ensure_scratch(h, sizeof(int64_t) * ((size_t)p->A.rows + 1)))) return st;
+        pref = (int64_t*)h->scratch;
+        if ((st = products_prefix(h, p->A, p->B, p->row_cnt, pref, p->scalars + 2))) return st;
+        if ((st = read_scalars(h, p->scalars + 2, 1, &p->P))) return st;
+    }
+    *num_products = p->P;
+    return SPG_STATUS_SUCCESS;
+}
+
+spg_status_t spg_symbolic(spg_handle_t h, spg_plan_t p, void* C_indptr, spg_index_t C_indptr_type,
+                          int64_t* nnzC) {
+    if (!h) return SPG_STATUS_NOT_INITIALIZED;
+    if (!p || !C_indptr || !nnzC) return SPG_STATUS_INVALID_VALUE;
+    if (C_indptr_type != SPG_INDEX_32I && C_indptr_type != SPG_INDEX_64I) return SPG_STATUS_INVALID_VALUE;
+    SPG_HIP(h, hipSetDevice(h->device));
+    spg_status_t st;
+    const bool i64 = p->A.indptr_type == SPG_INDEX_64I;
+    if (p->alg == SPG_ALG1) {
+        if (p->A.value_type == SPG_R_64F)
+            st = i64 ? alg1_compute<double, int64_t>(h, *p) : alg1_compute<double, int32_t>(h, *p);
+        else
+            st = i64 ? alg1_compute<float, int64_t>(h, *p) : alg1_compute<float, int32_t>(h, *p);
+    } else {
+        st = i64 ? symbolic_typed<int64_t>(h, *p) : symbolic_typed<int32_t>(h, *p);
+    }
+    if (st) return st;
+    st = C_indptr_type == SPG_INDEX_64I ? run_scan<int64_t>(h, *p, C_indptr)
+                                        : run_scan<int32_t>(h, *p, C_indptr);
+    if (st) return st;
+    int64_t sc[2];
+    if ((st = read_scalars(h, p->scalars, 2, sc))) return st;
+    if (sc[1]) return SPG_STATUS_OVERFLOW;
+    p->nnzC = sc[0];
+    p->c_indptr = C_indptr;
+    p->c_indptr_type = C_indptr_type;
+    *nnzC = sc[0];
+    return SPG_STATUS_SUCCESS;
+}
+
+spg_status_t spg_numeric(spg_handle_t h, spg_plan_t p, const void* alpha, spg_csr_t* C) {
+    if (!h) return SPG_STATUS_NOT_INITIALIZED;
+    if (!p || !alpha || !C) return SPG_STATUS_INVALID_VALUE;
+    if (p->nnzC < 0) return SPG_STATUS_NOT_INITIALIZED;     // spg_symbolic first
+    if (C->rows != p->A.rows || C->cols != p->B.cols) return SPG_STATUS_INVALID_VALUE;
+    if (C->value_type != p->A.value_type) return SPG_STATUS_INVALID_VALUE;
+    if (C->indptr != p->c_indptr || C->indptr_type != p->c_indptr_type) return SPG_STATUS_INVALID_VALUE;
+    if (C->nnz != p->nnzC) return SPG_STATUS_INVALID_VALUE;
+    if (p->nnzC > 0 && (!C->indices || !C->values)) return SPG_STATUS_INVALID_VALUE;
+    if (p->nnzC == 0) return SPG_STATUS_SUCCESS;
+    SPG_HIP(h, hipSetDevice(h->device));
+    const bool i64 = p->A.indptr_type == SPG_INDEX_64I;
+    const bool c64 = C->indptr_type == SPG_INDEX_64I;
+    if (p->A.value_type == SPG_R_64F) {
+        const double a = *(const double*)alpha;
+        if (i64) return c64 ? numeric_typed<double, int64_t, int64_t>(h, *p, *C, a)
+                            : numeric_typed<double, int64_t, int32_t>(h, *p, *C, a);
+        return c64 ? numeric_typed<double, int32_t, int64_t>(h, *p, *C, a)
+                   : numeric_typed<double, int32_t, int32_t>(h, *p, *C, a);
+    }
+    const float a = *(const float*)alpha;
+    if (i64) return c64 ? numeric_typed<float, int64_t, int64_t>(h, *p, *C, a)
+                        : numeric_typed<float, int64_t, int32_t>(h, *p, *C, a);
+    return c64 ? numeric_typed<float, int32_t, int64_t>(h, *p, *C, a)
+               : numeric_typed<float, int32_t, int32_t>(h, *p, *C, a);
+}
+
+spg_status_t spg_peak_bytes(spg_plan_t p, size_t* bytes) {
+    if (!p || !bytes) return SPG_STATUS_INVALID_VALUE;
+    const size_t ipc = p->nnzC >= 0 && p->c_indptr_type == SPG_INDEX_32I ? 4 : 8;
+    int64_t nnz = p->nnzC >= 0 ? p->nnzC : std::max<int64_t>(p->P, 0);
+    *bytes = p->ws_bytes + ipc * (size_t)(p->A.rows + 1) +
+             (size_t)nnz * (sizeof(int32_t) + vbytes(p->A.value_type));
+    return SPG_STATUS_SUCCESS;
+}
+
+spg_status_t spg_validate_csr(spg_handle_t h, const spg_csr_t* M, int* is_canonical) {
+    if (!h) return SPG_STATUS_NOT_INITIALIZED;
+    if (!is_canonical) return SPG_STATUS_INVALID_VALUE;
+    spg_status_t st = check_csr(M);
+    if (st) return st;
+    SPG_HIP(h, hipSetDevice(h->device));
+    if ((st = ensure_scratch(h, 256))) return st;
+    int* flags = (int*)h->scratch;
+    SPG_HIP(h, hipMemsetAsync(flags, 0, 2 * sizeof(int), h->stream));
+    st = M->indptr_type == SPG_INDEX_64I ? validate_typed<int64_t>(h, *M, flags)
+                                         : validate_typed<int32_t>(h, *M, flags);
+    if (st) return st;
+    SPG_HIP(h, hipMemcpyAsync(h->pinned, flags, 2 * sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    SPG_HIP(h, hipStreamSynchronize(h->stream));
+    const int* f = (const int*)h->pinned;
+    *is_canonical = f[1] ? -1 : (f[0] ? 0 : 1);
+    return SPG_STATUS_SUCCESS;
+}
+
+spg_status_t spg_plan_destroy(spg_plan_t p) {
+    if (!p) return SPG_STATUS_INVALID_VALUE;
+    delete p;
+    return SPG_STATUS_SUCCESS;
+}
+
+spg_status_t spg_set_timing(spg_handle_t h, int enable) {
+    if (!h) return SPG_STATUS_NOT_INITIALIZED;
+    SPG_HIP(h, hipStreamSynchronize(h->stream));
+    for (auto& q : h->pending) { h->pool.push_back(q.a); h->pool.push_back(q.b); }
+    h->pending.clear();
+    for (int i = 0; i < SPG_NUM_PHASES; ++i) { h->ms[i] = 0.0; h->launches[i] = 0; }
+    h->timing = enable != 0;
+    return SPG_STATUS_SUCCESS;
+}
+
+spg_status_t spg_get_timing(spg_handle_t h, spg_timing_t* t) {
+    if (!h) return SPG_STATUS_NOT_INITIALIZED;
+    if (!t) return SPG_STATUS_INVALID_VALUE;
+    for (auto& q : h->pending) {
+        SPG_HIP(h, hipEventSynchronize(q.b));
+        float ms = 0.0f;
+        SPG_HIP(h, hipEventElapsedTime(&ms, q.a, q.b));
+        h->ms[q.phase] += ms;
+        h->launches[q.phase] += 1;
+        h->pool.push_back(q.a);
+        h->pool.push_back(q.b);
+    }
+    h->pending.clear();
+    for (int i = 0; i < SPG_NUM_PHASES; ++i) { t->ms[i] = h->ms[i]; t->launches[i] = h->launches[i]; }
+    return SPG_STATUS_SUCCESS;
+}
+
+}  // extern "C"

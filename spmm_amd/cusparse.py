@@ -1,0 +1,198 @@
+"""``spgemm`` -- the drop-in for ``cupyx.cusparse.spgemm`` (the reference's hot-path
+boundary, modify_src/cupy-src/cupyx/cusparse.py:2007-2142), backed by libmi355_spgemm.so.
+
+Same signature, argument meaning and error behaviour as the reference:
+
+* ``RuntimeError('spgemm is not available.')`` when the engine cannot run
+  (``check_availability``, cusparse.py:169-186 / :2022-2023);
+* ``TypeError`` for a non-CSR operand (:2026-2029), ``ValueError('mismatched shape')``
+  (:2032-2033), ``assert a.has_canonical_format`` (:2030-2031);
+* dtype promotion of the operands (``_cast_common_type``, :52-56);
+* ``alg``: 1 -> ALG1 (single pass), 2 -> ALG2 (two phase), 3 -> ALG3 (chunked two phase,
+  uses ``chunk_fraction``), anything else -> the library default.  Note: the reference maps
+  ``alg=1`` to CUSPARSE_SPGEMM_DEFAULT (cusparse.py:2056-2057) while its C++ "ALG1" driver
+  uses CUSPARSE_SPGEMM_ALG1; here ``alg=1`` always means ALG1.
+* ``verbose`` prints the workspace size like the reference prints buff2 (:2106-2107).
+
+Device memory comes from torch's caching allocator on the current device; work runs on the
+current torch stream.  The result's ``indptr`` is int32 when nnz(C) < 2**31, int64 beyond.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import SpgCsr, SpgError, check
+from .sparse import csr_matrix
+
+_VT = {torch.float32: _lib.SPG_R_32F, torch.float64: _lib.SPG_R_64F}
+_IT = {torch.int32: _lib.SPG_INDEX_32I, torch.int64: _lib.SPG_INDEX_64I}
+_ALG = {1: _lib.SPG_ALG1, 2: _lib.SPG_ALG2, 3: _lib.SPG_ALG3}
+
+
+@dataclass
+class SpgemmStats:
+    """Accounting of the last spgemm call on this process (for the profilers)."""
+    alg: int = 0
+    workspace_bytes: int = 0
+    peak_bytes: int = 0        # workspace + C (spg_peak_bytes)
+    num_products: int = -1
+    nnz: int = 0
+
+
+last_stats = SpgemmStats()
+
+
+def check_availability(name: str) -> bool:
+    """True when the named routine can run here (a gfx950 device and the built library)."""
+    if name not in ("spgemm", "validate_csr"):
+        raise ValueError(f"No available version information specified for {name}")
+    try:
+        if not torch.cuda.is_available():
+            return False
+        _lib.get_handle(torch.cuda.current_device())
+        return True
+    except Exception:
+        return False
+
+
+def _csr_view(m: csr_matrix) -> SpgCsr:
+    return SpgCsr(m.shape[0], m.shape[1], m.nnz, m.indptr.data_ptr(),
+                  m.indices.data_ptr() if m.nnz else 0, m.data.data_ptr() if m.nnz else 0,
+                  _IT[m.indptr.dtype], _VT[m.data.dtype])
+
+
+def _handle_for(m: csr_matrix) -> _lib.Handle:
+    dev = m.device.index if m.device.index is not None else torch.cuda.current_device()
+    h = _lib.get_handle(dev)
+    h.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    return h
+
+
+def validate_csr(m: csr_matrix) -> int:
+    """1 canonical, 0 unsorted/duplicates, -1 malformed (spg_validate_csr)."""
+    if m.device.type != "cuda":
+        raise RuntimeError("validate_csr needs device-resident operands")
+    h = _handle_for(m)
+    v = _csr_view(m)
+    res = ctypes.c_int(0)
+    check(h.lib.spg_validate_csr(h.ptr, ctypes.byref(v), ctypes.byref(res)), "spg_validate_csr")
+    return res.value
+
+
+def _cast_common_type(a: csr_matrix, b: csr_matrix):
+    dt = np.promote_types(a.dtype, b.dtype)
+    if dt not in (np.float32, np.float64):
+        raise TypeError(f"spgemm supports float32/float64, got {dt}")
+    return a.astype(dt), b.astype(dt)
+
+
+def spgemm(a, b, alpha=1, alg=0, chunk_fraction=0.2, verbose=False):
+    """Matrix-matrix product for CSR matrices: ``C = alpha * A * B``.
+
+    Args:
+        a (csr_matrix): sparse matrix A (m x k), canonical format.
+        b (csr_matrix): sparse matrix B (k x n), canonical format.
+        alpha (scalar): coefficient.
+        alg (int): 1, 2, 3 select ALG1/ALG2/ALG3; other values the default.
+        chunk_fraction (float): ALG3 chunk size as a fraction of the products, (0, 1].
+        verbose (bool): print the workspace size.
+
+    Returns:
+        csr_matrix: C, with sorted column indices and structural entries kept.
+    """
+    if not check_availability("spgemm"):
+        raise RuntimeError("spgemm is not available.")
+    assert a.ndim == b.ndim == 2
+    if not isinstance(a, csr_matrix):
+        raise TypeError("unsupported type (actual: {})".format(type(a)))
+    if not isinstance(b, csr_matrix):
+        raise TypeError("unsupported type (actual: {})".format(type(b)))
+    assert a.has_canonical_format
+    assert b.has_canonical_format
+    if a.shape[1] != b.shape[0]:
+        raise ValueError("mismatched shape")
+    if a.device != b.device:
+        raise ValueError("operands are on different devices")
+
+    m, _ = a.shape
+    _, n = b.shape
+    a, b = _cast_common_type(a, b)
+    if a.indptr.dtype != b.indptr.dtype:   # the engine takes one row-pointer type for A and B
+        a = csr_matrix((a.data, a.indices, a.indptr.to(torch.int64)), shape=a.shape, canonical=True)
+        b = csr_matrix((b.data, b.indices, b.indptr.to(torch.int64)), shape=b.shape, canonical=True)
+        a.indptr, b.indptr = a.indptr.to(torch.int64), b.indptr.to(torch.int64)
+    algo = _ALG.get(alg, _lib.SPG_ALG_DEFAULT)
+    if algo == _lib.SPG_ALG3 and not (0.0 < float(chunk_fraction) <= 1.0):
+        raise ValueError(f"chunk_fraction must be in (0,1], got {chunk_fraction}")
+
+    dev = a.device
+    h = _handle_for(a)
+    lib = h.lib
+    va, vb = _csr_view(a), _csr_view(b)
+    ws_bytes = ctypes.c_size_t(0)
+    check(lib.spg_plan(h.ptr, ctypes.byref(va), ctypes.byref(vb), algo, float(chunk_fraction),
+                       ctypes.byref(ws_bytes), None, None), "spg_plan")
+    if verbose:
+        print("USING ALG", alg, "workspace GB =", ws_bytes.value / (1024 ** 3))
+    ws = torch.empty(max(ws_bytes.value, 1), dtype=torch.uint8, device=dev)
+    plan = ctypes.c_void_p()
+    check(lib.spg_plan(h.ptr, ctypes.byref(va), ctypes.byref(vb), algo, float(chunk_fraction),
+                       ctypes.byref(ws_bytes), ctypes.c_void_p(ws.data_ptr()),
+                       ctypes.byref(plan)), "spg_plan")
+    try:
+        indptr = torch.empty(m + 1, dtype=torch.int32, device=dev)
+        nnz = ctypes.c_int64(0)
+        st = lib.spg_symbolic(h.ptr, plan, ctypes.c_void_p(indptr.data_ptr()),
+                              _lib.SPG_INDEX_32I, ctypes.byref(nnz))
+        if st == _lib.STATUS_OVERFLOW:      # nnz(C) >= 2**31: redo the scan into int64
+            indptr = torch.empty(m + 1, dtype=torch.int64, device=dev)
+            st = lib.spg_symbolic(h.ptr, plan, ctypes.c_void_p(indptr.data_ptr()),
+                                  _lib.SPG_INDEX_64I, ctypes.byref(nnz))
+        check(st, "spg_symbolic")
+        nnzc = int(nnz.value)
+        indices = torch.empty(nnzc, dtype=torch.int32, device=dev)
+        data = torch.empty(nnzc, dtype=a.data.dtype, device=dev)
+        c = csr_matrix((data, indices, indptr), shape=(m, n), canonical=True)
+        c.indptr = indptr   # keep the int32/int64 choice made above
+        vc = _csr_view(c)
+        ctype = ctypes.c_double if a.data.dtype == torch.float64 else ctypes.c_float
+        al = ctype(float(alpha))
+        check(lib.spg_numeric(h.ptr, plan, ctypes.byref(al), ctypes.byref(vc)), "spg_numeric")
+        peak = ctypes.c_size_t(0)
+        lib.spg_peak_bytes(plan, ctypes.byref(peak))
+        last_stats.alg, last_stats.workspace_bytes = int(algo), int(ws_bytes.value)
+        last_stats.peak_bytes, last_stats.nnz = int(peak.value), nnzc
+        # keep the workspace alive until the queued kernels have consumed it
+        ws.record_stream(torch.cuda.current_stream(dev))
+        return c
+    finally:
+        lib.spg_plan_destroy(plan)
+
+
+def num_products(a: csr_matrix, b: csr_matrix) -> int:
+    """P = number of scalar products of A.B (cusparseSpGEMM_getNumProducts); GFLOPS = 2P/t."""
+    h = _handle_for(a)
+    va, vb = _csr_view(a), _csr_view(b)
+    ws_bytes = ctypes.c_size_t(0)
+    check(h.lib.spg_plan(h.ptr, ctypes.byref(va), ctypes.byref(vb), _lib.SPG_ALG2, 0.2,
+                         ctypes.byref(ws_bytes), None, None), "spg_plan")
+    ws = torch.empty(max(ws_bytes.value, 1), dtype=torch.uint8, device=a.device)
+    plan = ctypes.c_void_p()
+    check(h.lib.spg_plan(h.ptr, ctypes.byref(va), ctypes.byref(vb), _lib.SPG_ALG2, 0.2,
+                         ctypes.byref(ws_bytes), ctypes.c_void_p(ws.data_ptr()),
+                         ctypes.byref(plan)), "spg_plan")
+    try:
+        p = ctypes.c_int64(0)
+        check(h.lib.spg_num_products(h.ptr, plan, ctypes.byref(p)), "spg_num_products")
+        return int(p.value)
+    finally:
+        h.lib.spg_plan_destroy(plan)
+
+
+__all__ = ["spgemm", "check_availability", "num_products", "validate_csr", "SpgError",
+           "last_stats"]

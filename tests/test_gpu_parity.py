@@ -1,0 +1,235 @@
+"""Parity of the HIP SpGEMM (through the C ABI) with the CPU oracle and scipy.
+
+Bar: row pointers and column indices bit-exact; values bit-exact too, because
+the engine accumulates every C(i,j) in A's entry order with separately rounded mul/add,
+exactly scipy's rule (the fp tolerance of the north star, |c - c_ref| <= gamma_m (|A||B|)_ij,
+is therefore met with margin 0).  Structural zeros are kept (cuSPARSE semantics); after
+eliminate_zeros() the result must equal scipy's, array for array.
+"""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from oracle import oracle
+from tests.golden_cases import case_names, load
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+ALGS = [(1, 0.2), (2, 0.2), (3, 0.2), (3, 0.05), (0, 0.2)]
+
+
+def _dev():
+    return "cuda:0"
+
+
+def _gpu(A, B, alg=2, alpha=1.0, cf=0.2):
+    from spmm_amd import cusparse
+    from spmm_amd.sparse import csr_matrix
+    dA = csr_matrix(A, device=_dev())
+    dB = csr_matrix(B, device=_dev())
+    if not (dA.has_canonical_format and dB.has_canonical_format):
+        dA.sum_duplicates()
+        dB.sum_duplicates()
+    C = cusparse.spgemm(dA, dB, alpha=alpha, alg=alg, chunk_fraction=cf)
+    torch.cuda.synchronize()
+    return (C.indptr.cpu().numpy().astype(np.int64), C.indices.cpu().numpy(),
+            C.data.cpu().numpy(), C.shape)
+
+
+def _bits(x):
+    return x.view(np.uint32 if x.dtype == np.float32 else np.uint64)
+
+
+def _assert_same(got, ref):
+    p, j, x = got[:3]
+    rp, rj, rx = ref
+    assert np.array_equal(p, rp), "row pointer"
+    assert np.array_equal(j, rj), "column indices"
+    assert x.dtype == rx.dtype
+    assert np.array_equal(_bits(x), _bits(rx)), \
+        f"values differ at {np.flatnonzero(_bits(x) != _bits(rx))[:5]}"
+
+
+def _canon(A):
+    A = sp.csr_matrix(A, copy=True)
+    A.sum_duplicates()
+    return A
+
+
+@pytest.mark.parametrize("alg,cf", ALGS)
+@pytest.mark.parametrize("name", case_names())
+def test_golden_bitexact(name, alg, cf):
+    A, B, C, alpha = load(name)
+    got = _gpu(A, B, alg=alg, alpha=alpha, cf=cf)
+    # engine vs oracle (structural entries kept, sorted), on the canonicalised inputs
+    ref = oracle.spgemm(_canon(A), _canon(B), alpha=alpha, keep_zeros=True, sort=True)
+    _assert_same(got, ref)
+    if A.has_canonical_format and B.has_canonical_format:
+        # and vs scipy's own output (zeros dropped, columns sorted)
+        M = sp.csr_matrix((got[2], got[1], got[0]), shape=got[3])
+        M.eliminate_zeros()
+        Cs = C.copy()
+        Cs.sort_indices()
+        assert np.array_equal(M.indptr, Cs.indptr)
+        assert np.array_equal(M.indices, Cs.indices)
+        assert np.array_equal(_bits(M.data), _bits(Cs.data))
+    else:
+        np.testing.assert_allclose(sp.csr_matrix((got[2], got[1], got[0]), shape=got[3]).toarray(),
+                                   C.toarray(), rtol=1e-6, atol=0)
+
+
+@pytest.mark.parametrize("n,density,dtype", [
+    (1024, 0.01, np.float64), (2048, 0.02, np.float32), (16384, 1e-3, np.float64),
+    (8192, 1e-4, np.float64), (8192, 1e-3, np.float64), (4096, 0.05, np.float64),
+    (3000, 0.3, np.float32)])
+@pytest.mark.parametrize("alg", [1, 2, 3])
+def test_random_bitexact(n, density, dtype, alg):
+    from spmm_amd import gen
+    A, B = gen.scipy_pair(n, density, seed=n + int(density * 1e6), dtype=dtype, normal=True)
+    got = _gpu(A, B, alg=alg)
+    _assert_same(got, oracle.spgemm(A, B, keep_zeros=True, sort=True))
+
+
+def test_config2_nnz_and_products():
+    """BASELINE config 2: N=16384, density 1e-3, fp64, seed 42 (SURVEY 8d numbers)."""
+    from spmm_amd import cusparse, gen
+    from spmm_amd.sparse import csr_matrix
+    A, B = gen.scipy_pair(16384, 1e-3, seed=42)
+    dA, dB = csr_matrix(A, device=_dev()), csr_matrix(B, device=_dev())
+    assert cusparse.num_products(dA, dB) == 4402284
+    C = cusparse.spgemm(dA, dB, alg=1)
+    assert C.nnz == 4366124
+    _assert_same((C.indptr.cpu().numpy().astype(np.int64), C.indices.cpu().numpy(),
+                  C.data.cpu().numpy()), oracle.spgemm(A, B, keep_zeros=True, sort=True))
+
+
+def test_determinism_run_to_run():
+    """The reference's deterministic/ check, as a test: same inputs twice, same bits."""
+    from spmm_amd import gen
+    A, B = gen.scipy_pair(4096, 0.01, seed=2008, normal=True)
+    for alg in (1, 2, 3):
+        r1 = _gpu(A, B, alg=alg)
+        r2 = _gpu(A, B, alg=alg)
+        for a, b in zip(r1[:3], r2[:3]):
+            assert np.array_equal(a.view(np.uint8), b.view(np.uint8))
+
+
+def test_algs_agree_bitwise():
+    """numerical_error/error.py compares ALG1 with ALG3 (max abs error); here all three
+    algorithms must agree bit for bit for every chunk_fraction."""
+    from spmm_amd import gen
+    A, B = gen.scipy_pair(2048, 0.05, seed=10, dtype=np.float32, normal=True)
+    ref = _gpu(A, B, alg=1)
+    for alg, cf in [(2, 0.2), (3, 0.3), (3, 0.01), (3, 1.0)]:
+        _assert_same(_gpu(A, B, alg=alg, cf=cf), ref[:3])
+
+
+def test_dense_rows_multiwindow():
+    """Rows of C with more entries than one LDS window holds (window halving path) and
+    wide C (cursor walk over many windows)."""
+    rng = np.random.default_rng(1)
+    A = sp.random(64, 512, density=0.9, format="csr", random_state=rng)
+    B = sp.random(512, 6000, density=0.3, format="csr", random_state=rng)
+    A.sort_indices(); B.sort_indices()
+    for alg in (1, 2, 3):
+        _assert_same(_gpu(A, B, alg=alg), oracle.spgemm(A, B, keep_zeros=True, sort=True))
+    A = sp.random(200, 3000, density=0.05, format="csr", random_state=rng)
+    B = sp.random(3000, 400000, density=2e-4, format="csr", random_state=rng)
+    A.sort_indices(); B.sort_indices()
+    for alg in (1, 2):
+        _assert_same(_gpu(A, B, alg=alg), oracle.spgemm(A, B, keep_zeros=True, sort=True))
+
+
+def test_edge_shapes():
+    rng = np.random.default_rng(4)
+    cases = [
+        (sp.csr_matrix((0, 5)), sp.random(5, 7, density=0.5, format="csr", random_state=rng)),
+        (sp.random(6, 5, density=0.5, format="csr", random_state=rng), sp.csr_matrix((5, 0))),
+        (sp.random(6, 0, density=0.5, format="csr", random_state=rng), sp.csr_matrix((0, 9))),
+        (sp.random(1, 300, density=0.5, format="csr", random_state=rng),
+         sp.random(300, 1, density=0.5, format="csr", random_state=rng)),
+        (sp.csr_matrix(np.ones((3, 3))), sp.csr_matrix(np.eye(3))),
+    ]
+    for A, B in cases:
+        A = sp.csr_matrix(A, dtype=np.float64); B = sp.csr_matrix(B, dtype=np.float64)
+        A.sort_indices(); B.sort_indices()
+        for alg in (1, 2, 3):
+            got = _gpu(A, B, alg=alg)
+            _assert_same(got, oracle.spgemm(A, B, keep_zeros=True, sort=True))
+            assert got[3] == (A.shape[0], B.shape[1])
+
+
+def test_int64_row_pointers():
+    from spmm_amd import cusparse, gen
+    from spmm_amd.sparse import csr_matrix
+    A, B = gen.scipy_pair(2048, 0.01, seed=5)
+    dA, dB = csr_matrix(A, device=_dev()), csr_matrix(B, device=_dev())
+    dA.indptr = dA.indptr.to(torch.int64)
+    dB.indptr = dB.indptr.to(torch.int64)
+    C = cusparse.spgemm(dA, dB, alg=2)
+    _assert_same((C.indptr.cpu().numpy().astype(np.int64), C.indices.cpu().numpy(),
+                  C.data.cpu().numpy()), oracle.spgemm(A, B, keep_zeros=True, sort=True))
+
+
+def test_matmul_dispatch_and_formats():
+    """A @ B with CSR / CSC / COO right operands (CuPy _csr.py:151-184) and unsorted /
+    duplicate left operands (test_csr.py fixtures)."""
+    from spmm_amd.sparse import coo_matrix, csc_matrix, csr_matrix
+    A, B, _, _ = load("fixture_make_duplicate_f64")
+    x = B
+    for make in (lambda M: csr_matrix(M, device=_dev()), lambda M: csc_matrix(M, device=_dev()),
+                 lambda M: coo_matrix(M, device=_dev())):
+        dA = csr_matrix(A, device=_dev())
+        C = dA @ make(x)
+        np.testing.assert_allclose(C.toarray(), (A @ x).toarray(), rtol=1e-7, atol=0)
+
+
+def test_reference_error_behaviour():
+    """test_cusparse.py:413-454: TypeError for CSC, ValueError for mismatched shapes."""
+    from spmm_amd import cusparse
+    from spmm_amd.sparse import csc_matrix, csr_matrix
+    rng = np.random.default_rng(0)
+    a = sp.random(2, 4, density=0.5, dtype=np.float32, random_state=rng)
+    b = sp.random(4, 3, density=0.5, dtype=np.float32, random_state=rng)
+    with pytest.raises(TypeError):
+        cusparse.spgemm(csc_matrix(a, device=_dev()), csr_matrix(b, device=_dev()))
+    with pytest.raises(TypeError):
+        cusparse.spgemm(csr_matrix(a, device=_dev()), csc_matrix(b, device=_dev()))
+    with pytest.raises(ValueError):
+        cusparse.spgemm(csc_matrix(a, device=_dev()).T, csr_matrix(b, device=_dev()))
+    with pytest.raises(ValueError):
+        cusparse.spgemm(csr_matrix(a, device=_dev()), csc_matrix(b, device=_dev()).T)
+    assert cusparse.check_availability("spgemm")
+
+
+def test_upstream_testspgemm_alpha():
+    """test_cusparse.py:372-411: f32/f64, shapes (2,3,4), (4,3,2) and the (100000, 100000,
+    50) run-only case, alpha = 0.5."""
+    from spmm_amd import cusparse
+    from spmm_amd.sparse import csr_matrix
+    for dt in (np.float32, np.float64):
+        for (m, n, k) in [(2, 3, 4), (4, 3, 2), (100000, 100000, 50)]:
+            rng = np.random.default_rng(m + n + k)
+            a = sp.random(m, k, density=0.5, dtype=dt, random_state=rng, format="csr")
+            b = sp.random(k, n, density=0.5, dtype=dt, random_state=rng, format="csr")
+            a.sort_indices(); b.sort_indices()
+            c = cusparse.spgemm(csr_matrix(a, device=_dev()), csr_matrix(b, device=_dev()),
+                                alpha=0.5)
+            if m == 100000:
+                assert c.nnz > 0
+                continue
+            np.testing.assert_array_almost_equal(c.toarray(), (0.5 * a.dot(b)).toarray())
+
+
+def test_validate_csr():
+    from spmm_amd import cusparse
+    from spmm_amd.sparse import csr_matrix
+    for name, want in [("fixture_make_unordered_f64", 0), ("fixture_make_duplicate_f64", 0),
+                       ("config1_n1024_d0.01_f64", 1)]:
+        A, _, _, _ = load(name)
+        d = csr_matrix((A.data, A.indices, A.indptr), shape=A.shape, device=_dev())
+        assert cusparse.validate_csr(d) == want
+    bad = csr_matrix((np.ones(2), np.array([0, 9], np.int32), np.array([0, 1, 2])),
+                     shape=(2, 4), device=_dev())
+    assert cusparse.validate_csr(bad) == -1
