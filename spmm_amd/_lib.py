@@ -40,7 +40,11 @@ STATUS_OVERFLOW = 100
 # every symbol include/spgemm.h declares (tests/test_abi.py checks the .so exports them)
 EXPORTS = ("spg_version", "spg_status_string", "spg_create", "spg_destroy", "spg_set_stream",
            "spg_last_hip_error", "spg_plan", "spg_num_products", "spg_symbolic",
-           "spg_numeric", "spg_peak_bytes", "spg_validate_csr", "spg_plan_destroy")
+           "spg_numeric", "spg_peak_bytes", "spg_validate_csr", "spg_plan_destroy",
+           "spg_set_timing", "spg_get_timing")
+
+PHASES = ("products", "scan", "symbolic", "numeric", "compact", "validate")
+NUM_PHASES = 8
 
 
 class SpgCsr(ctypes.Structure):
@@ -49,6 +53,11 @@ class SpgCsr(ctypes.Structure):
                 ("indptr", ctypes.c_void_p), ("indices", ctypes.c_void_p),
                 ("values", ctypes.c_void_p), ("indptr_type", ctypes.c_int),
                 ("value_type", ctypes.c_int)]
+
+
+class SpgTiming(ctypes.Structure):
+    """spg_timing_t"""
+    _fields_ = [("ms", ctypes.c_double * 8), ("launches", ctypes.c_int64 * 8)]
 
 
 class SpgError(RuntimeError):
@@ -94,6 +103,8 @@ def load():
             "spg_peak_bytes": (ctypes.c_int, [vp, ctypes.POINTER(sz)]),
             "spg_validate_csr": (ctypes.c_int, [vp, csrp, ctypes.POINTER(ctypes.c_int)]),
             "spg_plan_destroy": (ctypes.c_int, [vp]),
+            "spg_set_timing": (ctypes.c_int, [vp, ctypes.c_int]),
+            "spg_get_timing": (ctypes.c_int, [vp, ctypes.POINTER(SpgTiming)]),
         }
         for name, (res, args) in proto.items():
             fn = getattr(lib, name)
@@ -121,6 +132,15 @@ class Handle:
 
     def set_stream(self, stream_ptr: int) -> None:
         check(self.lib.spg_set_stream(self.ptr, ctypes.c_void_p(stream_ptr)), "spg_set_stream")
+
+    def set_timing(self, enable: bool) -> None:
+        check(self.lib.spg_set_timing(self.ptr, int(enable)), "spg_set_timing")
+
+    def get_timing(self) -> dict:
+        """{phase: (total device ms, launches)} accumulated since set_timing(True)."""
+        t = SpgTiming()
+        check(self.lib.spg_get_timing(self.ptr, ctypes.byref(t)), "spg_get_timing")
+        return {name: (t.ms[i], int(t.launches[i])) for i, name in enumerate(PHASES)}
 
     def __del__(self):
         try:

@@ -31,6 +31,13 @@ struct spg_handle_s {
     std::vector<hipEvent_t> pool;
     double ms[SPG_NUM_PHASES] = {};
     int64_t launches[SPG_NUM_PHASES] = {};
+    // what the last size query measured (see spg_plan)
+    bool q_valid = false;
+    spg_csr_t q_A{}, q_B{};
+    spg_alg_t q_alg = SPG_ALG2;
+    float q_cf = 0.f;
+    int64_t q_P = -1, q_seg_len = 0;
+    std::vector<int64_t> q_chunk_rows, q_chunk_nz;
 };
 
 struct spg_plan_s {
@@ -51,6 +58,10 @@ struct spg_plan_s {
     int64_t nnzC = -1;
     void* c_indptr = nullptr;
     spg_index_t c_indptr_type = SPG_INDEX_32I;
+    int32_t* spill = nullptr;       // rows the short-row kernel hands to the general kernel
+    unsigned long long* scan_status = nullptr;   // look-back scan: ticket + one word per tile
+    bool use_short = false;         // dispatch the short-row kernel first
+    int symbolic_runs = 0;          // spg_symbolic may be called again (e.g. int32 -> int64)
     std::vector<int64_t> chunk_rows;   // ALG3 row boundaries (chunk c = [r[c], r[c+1]))
     std::vector<int64_t> chunk_nz;     // A entry offset of each boundary
 };
@@ -63,6 +74,22 @@ inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 inline size_t vbytes(spg_dtype_t t) { return t == SPG_R_64F ? 8 : 4; }
 
 inline int64_t grid_for(int64_t rows, int per_block) { return (rows + per_block - 1) / per_block; }
+
+inline int64_t scan_tiles(int64_t n) { return n > 0 ? (n + SCAN_TILE - 1) / SCAN_TILE : 1; }
+
+// Rows of the expected shape go to the short-row kernel first; the rest (and every row it
+// rejects) to the general windowed kernels.  Only a scheduling choice: results are the
+// same either way.
+inline bool want_short(const spg_csr_t& A, const spg_csr_t& B) {
+    if (B.cols > 32LL * ShortSmall::NW || A.rows == 0) return false;
+    const double avgA = (double)A.nnz / (double)A.rows;
+    const double avgB = B.rows > 0 ? (double)B.nnz / (double)B.rows : 0.0;
+    return avgA <= 48.0 && avgA * avgB <= 400.0;
+}
+
+// grid of a list-mode general kernel: enough waves to cover the spilled rows of a
+// launch over `rows` rows, capped (the waves loop over the list)
+inline unsigned list_grid(int64_t rows) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>(grid_for(rows, WPB), 1024)); }
 
 spg_status_t hip_fail(spg_handle_t h, hipError_t e) {
     if (h) h->last_hip = (int)e;
@@ -133,9 +160,24 @@ spg_status_t ensure_scratch(spg_handle_t h, size_t bytes) {
 }
 
 // Product prefix of every row into `pref` (rows + 1 int64) and its total into scal[0].
+// `status` (tiles + 1 words) must be zero: plans zero theirs once when they are built
+template <typename OUT>
+spg_status_t launch_scan(spg_handle_t h, int64_t n, const int64_t* in, OUT* out,
+                         unsigned long long* status, int64_t* scal, bool zero_status) {
+    const int64_t tiles = scan_tiles(n);
+    if (zero_status)
+        SPG_HIP(h, hipMemsetAsync(status, 0, sizeof(unsigned long long) * (size_t)(tiles + 1), h->stream));
+    PhaseTimer pt(h, SPG_PHASE_SCAN);
+    hipLaunchKernelGGL(k_scan_lb<OUT>, dim3((unsigned)tiles), dim3(BLOCK), 0, h->stream, n, in, out,
+                       status, scal);
+    SPG_LAUNCHED(h);
+    return SPG_STATUS_SUCCESS;
+}
+
 template <typename IP>
 spg_status_t launch_products(spg_handle_t h, const spg_csr_t& A, const spg_csr_t& B,
-                             int64_t* cnt, int64_t* pref, int64_t* scal) {
+                             int64_t* cnt, int64_t* pref, int64_t* scal,
+                             unsigned long long* status, bool zero_status) {
     const int64_t rows = A.rows;
     if (rows > 0) {
         PhaseTimer pt(h, SPG_PHASE_PRODUCTS);
@@ -144,17 +186,33 @@ spg_status_t launch_products(spg_handle_t h, const spg_csr_t& A, const spg_csr_t
                            (const IP*)B.indptr, cnt);
         SPG_LAUNCHED(h);
     }
-    PhaseTimer pt(h, SPG_PHASE_SCAN);
-    hipLaunchKernelGGL(k_scan_excl<int64_t>, dim3(1), dim3(1024), 0, h->stream, rows,
-                       (const int64_t*)cnt, pref, scal);
-    SPG_LAUNCHED(h);
-    return SPG_STATUS_SUCCESS;
+    return launch_scan<int64_t>(h, rows, cnt, pref, status, scal, zero_status);
 }
 
 spg_status_t products_prefix(spg_handle_t h, const spg_csr_t& A, const spg_csr_t& B,
-                             int64_t* cnt, int64_t* pref, int64_t* scal) {
-    return A.indptr_type == SPG_INDEX_64I ? launch_products<int64_t>(h, A, B, cnt, pref, scal)
-                                          : launch_products<int32_t>(h, A, B, cnt, pref, scal);
+                             int64_t* cnt, int64_t* pref, int64_t* scal,
+                             unsigned long long* status, bool zero_status = true) {
+    return A.indptr_type == SPG_INDEX_64I ? launch_products<int64_t>(h, A, B, cnt, pref, scal, status, zero_status)
+                                          : launch_products<int32_t>(h, A, B, cnt, pref, scal, status, zero_status);
+}
+
+// handle scratch for plan-time product prefixes: cnt[rows] | pref[rows+1] | scal[16] | status
+struct ScratchView {
+    int64_t* cnt;
+    int64_t* pref;
+    int64_t* scal;
+    unsigned long long* status;
+};
+
+spg_status_t scratch_for_products(spg_handle_t h, int64_t rows, ScratchView& v) {
+    const size_t words = 2 * (size_t)rows + 1 + 16 + (size_t)scan_tiles(rows) + 1;
+    spg_status_t st = ensure_scratch(h, sizeof(int64_t) * words);
+    if (st) return st;
+    v.cnt = (int64_t*)h->scratch;
+    v.pref = v.cnt + rows;
+    v.scal = v.pref + rows + 1;
+    v.status = (unsigned long long*)(v.scal + 16);
+    return SPG_STATUS_SUCCESS;
 }
 
 spg_status_t read_scalars(spg_handle_t h, const int64_t* dev, int n, int64_t* out) {
@@ -165,15 +223,17 @@ spg_status_t read_scalars(spg_handle_t h, const int64_t* dev, int n, int64_t* ou
 }
 
 struct Layout {
-    size_t scalars = 0, row_cnt = 0, seg = 0, ub = 0, tj = 0, tx = 0, total = 0;
+    size_t scalars = 0, row_cnt = 0, seg = 0, spill = 0, status = 0, ub = 0, tj = 0, tx = 0, total = 0;
 };
 
 Layout make_layout(const spg_plan_s& p) {
     Layout L;
     size_t off = 0;
     L.scalars = off; off = align_up(off + 16 * sizeof(int64_t));
+    L.status = off;  off = align_up(off + sizeof(unsigned long long) * 2 * (size_t)(scan_tiles(p.A.rows) + 1));
     L.row_cnt = off; off = align_up(off + sizeof(int64_t) * (size_t)(p.A.rows + 1));
     L.seg = off;     off = align_up(off + sizeof(uint32_t) * 2 * (size_t)std::max<int64_t>(p.seg_len, 1));
+    L.spill = off;   off = align_up(off + sizeof(int32_t) * 2 * (size_t)std::max<int64_t>(p.A.rows, 1));
     if (p.alg == SPG_ALG1) {
         L.ub = off; off = align_up(off + sizeof(int64_t) * (size_t)(p.A.rows + 1));
         L.tj = off; off = align_up(off + sizeof(int32_t) * (size_t)std::max<int64_t>(p.P, 1));
@@ -187,6 +247,8 @@ void carve(spg_plan_s& p, const Layout& L) {
     p.scalars = (int64_t*)(p.ws + L.scalars);
     p.row_cnt = (int64_t*)(p.ws + L.row_cnt);
     p.seg = (uint32_t*)(p.ws + L.seg);
+    p.spill = (int32_t*)(p.ws + L.spill);
+    p.scan_status = (unsigned long long*)(p.ws + L.status);
     if (p.alg == SPG_ALG1) {
         p.ub = (int64_t*)(p.ws + L.ub);
         p.tj = (int32_t*)(p.ws + L.tj);
@@ -201,12 +263,11 @@ spg_status_t plan_chunks(spg_handle_t h, spg_plan_s& p) {
     p.chunk_nz.assign({0, p.A.nnz});
     p.seg_len = p.A.nnz;
     if (rows == 0) return SPG_STATUS_SUCCESS;
-    spg_status_t st = ensure_scratch(h, sizeof(int64_t) * (2 * (size_t)rows + 18));
+    ScratchView sv;
+    spg_status_t st = scratch_for_products(h, rows, sv);
     if (st) return st;
-    int64_t* cnt = (int64_t*)h->scratch;
-    int64_t* pref = cnt + rows;
-    int64_t* scal = pref + rows + 1;
-    if ((st = products_prefix(h, p.A, p.B, cnt, pref, scal))) return st;
+    int64_t* pref = sv.pref;
+    if ((st = products_prefix(h, p.A, p.B, sv.cnt, sv.pref, sv.scal, sv.status))) return st;
     std::vector<int64_t> hp((size_t)rows + 1), ha((size_t)rows + 1);
     SPG_HIP(h, hipMemcpyAsync(hp.data(), pref, sizeof(int64_t) * (rows + 1), hipMemcpyDeviceToHost, h->stream));
     if (p.A.indptr_type == SPG_INDEX_64I) {
@@ -242,14 +303,48 @@ spg_status_t plan_chunks(spg_handle_t h, spg_plan_s& p) {
 }
 
 // --------------------------------------------------------------------- typed launchers
+// Spill chain of the short-row path: small rows -> list 1 -> medium rows -> list 2 ->
+// general windowed kernel.  Counters live in scalars[4] (int32 x2).
+// scalars[4]: two int32 spill counters of the symbolic phase; scalars[5]: of the numeric
+// phase.  The whole control block (scalars + scan status words) is zeroed once per plan.
+inline int32_t* spill_counts(spg_plan_s& p, bool numeric) {
+    return (int32_t*)(p.scalars + (numeric ? 5 : 4));
+}
+
 template <typename IP>
 spg_status_t run_symbolic_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_t r1, int64_t nz0) {
     const int64_t n = r1 - r0;
     if (n <= 0) return SPG_STATUS_SUCCESS;
+    const IP* Ap = (const IP*)p.A.indptr;
+    const IP* Bp = (const IP*)p.B.indptr;
+    const int32_t* Aj = (const int32_t*)p.A.indices;
+    const int32_t* Bj = (const int32_t*)p.B.indices;
     PhaseTimer pt(h, SPG_PHASE_SYMBOLIC);
-    hipLaunchKernelGGL(k_symbolic<IP>, dim3((unsigned)grid_for(n, WPB)), dim3(BLOCK), 0, h->stream,
-                       r0, n, p.B.cols, (const IP*)p.A.indptr, (const int32_t*)p.A.indices,
-                       (const IP*)p.B.indptr, (const int32_t*)p.B.indices, p.row_cnt, p.seg, nz0);
+    if (p.use_short) {
+        int32_t* cnt = spill_counts(p, false);
+        int32_t* l1 = p.spill;
+        int32_t* l2 = p.spill + p.A.rows;
+        hipLaunchKernelGGL((k_short<double, IP, int64_t, SHORT_SYM, ShortSmall>),
+                           dim3((unsigned)grid_for(n, ShortSmall::WPB)), dim3(ShortSmall::WPB * WAVE), 0,
+                           h->stream, r0, n, p.B.cols, Ap, Aj, (const double*)nullptr, Bp, Bj,
+                           (const double*)nullptr, (const int64_t*)nullptr, (int32_t*)nullptr,
+                           (double*)nullptr, 1.0, p.row_cnt, l1, cnt, (const int32_t*)nullptr,
+                           (const int32_t*)nullptr);
+        SPG_LAUNCHED(h);
+        hipLaunchKernelGGL((k_short<double, IP, int64_t, SHORT_SYM, ShortMedium>), dim3(list_grid(std::min<int64_t>(n, 256))),
+                           dim3(ShortMedium::WPB * WAVE), 0, h->stream, r0, n, p.B.cols, Ap, Aj,
+                           (const double*)nullptr, Bp, Bj, (const double*)nullptr, (const int64_t*)nullptr,
+                           (int32_t*)nullptr, (double*)nullptr, 1.0, p.row_cnt, l2, cnt + 1,
+                           (const int32_t*)l1, (const int32_t*)cnt);
+        SPG_LAUNCHED(h);
+        hipLaunchKernelGGL(k_symbolic<IP>, dim3(list_grid(std::min<int64_t>(n, 256))), dim3(BLOCK), 0, h->stream, r0, n,
+                           p.B.cols, Ap, Aj, Bp, Bj, p.row_cnt, p.seg, nz0, (const int32_t*)l2,
+                           (const int32_t*)(cnt + 1));
+    } else {
+        hipLaunchKernelGGL(k_symbolic<IP>, dim3((unsigned)grid_for(n, WPB)), dim3(BLOCK), 0, h->stream,
+                           r0, n, p.B.cols, Ap, Aj, Bp, Bj, p.row_cnt, p.seg, nz0,
+                           (const int32_t*)nullptr, (const int32_t*)nullptr);
+    }
     SPG_LAUNCHED(h);
     return SPG_STATUS_SUCCESS;
 }
@@ -259,43 +354,67 @@ spg_status_t run_numeric_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_t
                               const OFF* off, int32_t* cj, T* cx, T alpha) {
     const int64_t n = r1 - r0;
     if (n <= 0) return SPG_STATUS_SUCCESS;
+    const IP* Ap = (const IP*)p.A.indptr;
+    const IP* Bp = (const IP*)p.B.indptr;
+    const int32_t* Aj = (const int32_t*)p.A.indices;
+    const int32_t* Bj = (const int32_t*)p.B.indices;
+    const T* Ax = (const T*)p.A.values;
+    const T* Bx = (const T*)p.B.values;
+    constexpr int MODE = UB ? SHORT_NUMUB : SHORT_NUM;
     PhaseTimer pt(h, SPG_PHASE_NUMERIC);
-    hipLaunchKernelGGL((k_numeric<T, IP, OFF, UB>), dim3((unsigned)grid_for(n, WPB)), dim3(BLOCK), 0,
-                       h->stream, r0, n, p.B.cols, (const IP*)p.A.indptr,
-                       (const int32_t*)p.A.indices, (const T*)p.A.values, (const IP*)p.B.indptr,
-                       (const int32_t*)p.B.indices, (const T*)p.B.values, off, cj, cx, alpha,
-                       p.row_cnt, p.seg, nz0, p.seg_len);
+    if (p.use_short) {
+        int32_t* cnt = spill_counts(p, true);
+        int32_t* l1 = p.spill;
+        int32_t* l2 = p.spill + p.A.rows;
+        hipLaunchKernelGGL((k_short<T, IP, OFF, MODE, ShortSmall>), dim3((unsigned)grid_for(n, ShortSmall::WPB)),
+                           dim3(ShortSmall::WPB * WAVE), 0, h->stream, r0, n, p.B.cols, Ap, Aj, Ax, Bp, Bj,
+                           Bx, off, cj, cx, alpha, p.row_cnt, l1, cnt, (const int32_t*)nullptr,
+                           (const int32_t*)nullptr);
+        SPG_LAUNCHED(h);
+        hipLaunchKernelGGL((k_short<T, IP, OFF, MODE, ShortMedium>), dim3(list_grid(std::min<int64_t>(n, 256))),
+                           dim3(ShortMedium::WPB * WAVE), 0, h->stream, r0, n, p.B.cols, Ap, Aj, Ax, Bp,
+                           Bj, Bx, off, cj, cx, alpha, p.row_cnt, l2, cnt + 1, (const int32_t*)l1,
+                           (const int32_t*)cnt);
+        SPG_LAUNCHED(h);
+        hipLaunchKernelGGL((k_numeric<T, IP, OFF, UB>), dim3(list_grid(std::min<int64_t>(n, 256))), dim3(BLOCK), 0, h->stream,
+                           r0, n, p.B.cols, Ap, Aj, Ax, Bp, Bj, Bx, off, cj, cx, alpha, p.row_cnt,
+                           p.seg, nz0, p.seg_len, (const int32_t*)l2, (const int32_t*)(cnt + 1));
+    } else {
+        hipLaunchKernelGGL((k_numeric<T, IP, OFF, UB>), dim3((unsigned)grid_for(n, WPB)), dim3(BLOCK), 0,
+                           h->stream, r0, n, p.B.cols, Ap, Aj, Ax, Bp, Bj, Bx, off, cj, cx, alpha,
+                           p.row_cnt, p.seg, nz0, p.seg_len, (const int32_t*)nullptr,
+                           (const int32_t*)nullptr);
+    }
     SPG_LAUNCHED(h);
     return SPG_STATUS_SUCCESS;
 }
 
 template <typename OUT>
 spg_status_t run_scan(spg_handle_t h, spg_plan_s& p, void* out) {
-    PhaseTimer pt(h, SPG_PHASE_SCAN);
-    hipLaunchKernelGGL(k_scan_excl<OUT>, dim3(1), dim3(1024), 0, h->stream, p.A.rows,
-                       (const int64_t*)p.row_cnt, (OUT*)out, p.scalars);
-    SPG_LAUNCHED(h);
-    return SPG_STATUS_SUCCESS;
+    // the row-pointer scan uses the second status region of the control block
+    return launch_scan<OUT>(h, p.A.rows, (const int64_t*)p.row_cnt, (OUT*)out,
+                            p.scan_status + scan_tiles(p.A.rows) + 1, p.scalars, false);
 }
 
 template <typename IP>
 spg_status_t symbolic_typed(spg_handle_t h, spg_plan_s& p) {
     spg_status_t st;
     if (p.alg == SPG_ALG3) {
-        for (size_t c = 0; c + 1 < p.chunk_rows.size(); ++c)
+        for (size_t c = 0; c + 1 < p.chunk_rows.size(); ++c) {
+            if (c > 0 && p.use_short)
+                SPG_HIP(h, hipMemsetAsync(spill_counts(p, false), 0, 2 * sizeof(int32_t), h->stream));
             if ((st = run_symbolic_rows<IP>(h, p, p.chunk_rows[c], p.chunk_rows[c + 1], p.chunk_nz[c])))
                 return st;
+        }
         return SPG_STATUS_SUCCESS;
     }
-    int64_t nz0 = 0;
-    return run_symbolic_rows<IP>(h, p, 0, p.A.rows, nz0);
+    return run_symbolic_rows<IP>(h, p, 0, p.A.rows, 0);
 }
 
 template <typename T, typename IP>
 spg_status_t alg1_compute(spg_handle_t h, spg_plan_s& p) {
-    // upper-bound offsets = product prefix, then the fused structure+value pass
-    spg_status_t st = products_prefix(h, p.A, p.B, p.row_cnt, p.ub, p.scalars);
-    if (st) return st;
+    // the fused structure+value pass at upper-bound offsets (the product prefix in p.ub,
+    // computed when the plan was built)
     return run_numeric_rows<T, IP, int64_t, true>(h, p, 0, p.A.rows, 0, p.ub, p.tj, (T*)p.tx, (T)1);
 }
 
@@ -314,11 +433,14 @@ spg_status_t numeric_typed(spg_handle_t h, spg_plan_s& p, const spg_csr_t& C, T 
     }
     spg_status_t st;
     if (p.alg == SPG_ALG3) {
-        for (size_t c = 0; c + 1 < p.chunk_rows.size(); ++c)
+        for (size_t c = 0; c + 1 < p.chunk_rows.size(); ++c) {
+            if (c > 0 && p.use_short)
+                SPG_HIP(h, hipMemsetAsync(spill_counts(p, true), 0, 2 * sizeof(int32_t), h->stream));
             if ((st = run_numeric_rows<T, IP, IPC, false>(h, p, p.chunk_rows[c], p.chunk_rows[c + 1],
                                                           p.chunk_nz[c], cp, (int32_t*)C.indices,
                                                           (T*)C.values, alpha)))
                 return st;
+        }
         return SPG_STATUS_SUCCESS;
     }
     return run_numeric_rows<T, IP, IPC, false>(h, p, 0, p.A.rows, 0, cp, (int32_t*)C.indices,
@@ -431,16 +553,42 @@ spg_status_t spg_plan(spg_handle_t h, const spg_csr_t* A, const spg_csr_t* B, sp
     tmp.alg = alg == SPG_ALG_DEFAULT ? SPG_ALG2 : alg;
     tmp.cf = chunk_fraction;
     tmp.seg_len = A->nnz;
+    tmp.use_short = want_short(*A, *B);
+    // ALG1 and ALG3 size their buffers / chunks from the product counts, which needs the
+    // device once.  The size query and the building call of one plan see the same
+    // operands, so the building call reuses what the query measured.
+    const bool same_as_query = h->q_valid && h->q_alg == tmp.alg && h->q_cf == chunk_fraction &&
+                               std::memcmp(&h->q_A, A, sizeof(spg_csr_t)) == 0 &&
+                               std::memcmp(&h->q_B, B, sizeof(spg_csr_t)) == 0;
     if (tmp.alg == SPG_ALG1) {
-        // size the upper-bound buffers from the exact product count (waits for the device)
-        if ((st = ensure_scratch(h, sizeof(int64_t) * (2 * (size_t)A->rows + 18)))) return st;
-        int64_t* cnt = (int64_t*)h->scratch;
-        int64_t* pref = cnt + A->rows;
-        int64_t* scal = pref + A->rows + 1;
-        if ((st = products_prefix(h, *A, *B, cnt, pref, scal))) return st;
-        if ((st = read_scalars(h, scal, 1, &tmp.P))) return st;
+        if (workspace && same_as_query) {
+            tmp.P = h->q_P;
+        } else {
+            ScratchView sv;
+            if ((st = scratch_for_products(h, A->rows, sv))) return st;
+            if ((st = products_prefix(h, *A, *B, sv.cnt, sv.pref, sv.scal, sv.status))) return st;
+            if ((st = read_scalars(h, sv.scal, 1, &tmp.P))) return st;
+        }
     } else if (tmp.alg == SPG_ALG3) {
-        if ((st = plan_chunks(h, tmp))) return st;
+        if (workspace && same_as_query) {
+            tmp.P = h->q_P;
+            tmp.chunk_rows = h->q_chunk_rows;
+            tmp.chunk_nz = h->q_chunk_nz;
+            tmp.seg_len = h->q_seg_len;
+        } else if ((st = plan_chunks(h, tmp))) {
+            return st;
+        }
+    }
+    if (!workspace) {
+        h->q_valid = true;
+        h->q_A = *A;
+        h->q_B = *B;
+        h->q_alg = tmp.alg;
+        h->q_cf = chunk_fraction;
+        h->q_P = tmp.P;
+        h->q_chunk_rows = tmp.chunk_rows;
+        h->q_chunk_nz = tmp.chunk_nz;
+        h->q_seg_len = tmp.seg_len;
     }
     const Layout L = make_layout(tmp);
     if (!workspace) {
@@ -453,6 +601,17 @@ spg_status_t spg_plan(spg_handle_t h, const spg_csr_t* A, const spg_csr_t* B, sp
     p->ws = (char*)workspace;
     p->ws_bytes = *workspace_bytes;
     carve(*p, L);
+    // control block: scalars + spill counters + scan status words, zeroed once per plan
+    {
+        hipError_t e1 = hipMemsetAsync(p->ws, 0, L.row_cnt, h->stream);   // scalars + status
+        if (e1 != hipSuccess) { delete p; return hip_fail(h, e1); }
+    }
+    if (p->alg == SPG_ALG1) {
+        // upper-bound offsets for the single pass: product prefix straight into the workspace
+        spg_status_t st2 = products_prefix(h, p->A, p->B, p->row_cnt, p->ub, p->scalars + 2,
+                                           p->scan_status, false);
+        if (st2) { delete p; return st2; }
+    }
     *plan = p;
     return SPG_STATUS_SUCCESS;
 }
@@ -463,12 +622,10 @@ spg_status_t spg_num_products(spg_handle_t h, spg_plan_t p, int64_t* num_product
     if (p->P < 0) {
         SPG_HIP(h, hipSetDevice(h->device));
         spg_status_t st;
-        // row_cnt doubles as the per-row count buffer; scalars[2] receives the total
-        int64_t* pref = (int64_t*)h->scratch;
-        if ((st = ensure_scratch(h, sizeof(int64_t) * ((size_t)p->A.rows + 1)))) return st;
-        pref = (int64_t*)h->scratch;
-        if ((st = products_prefix(h, p->A, p->B, p->row_cnt, pref, p->scalars + 2))) return st;
-        if ((st = read_scalars(h, p->scalars + 2, 1, &p->P))) return st;
+        ScratchView sv;
+        if ((st = scratch_for_products(h, p->A.rows, sv))) return st;
+        if ((st = products_prefix(h, p->A, p->B, sv.cnt, sv.pref, sv.scal, sv.status))) return st;
+        if ((st = read_scalars(h, sv.scal, 1, &p->P))) return st;
     }
     *num_products = p->P;
     return SPG_STATUS_SUCCESS;
@@ -482,6 +639,13 @@ spg_status_t spg_symbolic(spg_handle_t h, spg_plan_t p, void* C_indptr, spg_inde
     SPG_HIP(h, hipSetDevice(h->device));
     spg_status_t st;
     const bool i64 = p->A.indptr_type == SPG_INDEX_64I;
+    if (p->symbolic_runs++ > 0) {
+        // a repeated call (e.g. retrying with int64 row pointers): re-arm the spill counters
+        // and the row-pointer scan's status words
+        const int64_t tiles = scan_tiles(p->A.rows) + 1;
+        SPG_HIP(h, hipMemsetAsync(p->scalars + 4, 0, 2 * sizeof(int64_t), h->stream));
+        SPG_HIP(h, hipMemsetAsync(p->scan_status + tiles, 0, sizeof(unsigned long long) * tiles, h->stream));
+    }
     if (p->alg == SPG_ALG1) {
         if (p->A.value_type == SPG_R_64F)
             st = i64 ? alg1_compute<double, int64_t>(h, *p) : alg1_compute<double, int32_t>(h, *p);

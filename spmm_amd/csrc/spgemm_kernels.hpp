@@ -31,115 +31,75 @@ __global__ __launch_bounds__(BLOCK) void k_row_products(int64_t rows, const IP* 
 }
 
 // ---------------------------------------------------------------------------------------
-// Exclusive scan of in[0..n) into out[0..n], out[n] = total; scalars[0] = total,
-// scalars[1] = 1 if the total does not fit OUT.  One block of 1024 threads, 8 items each.
-template <typename OUT>
-__global__ __launch_bounds__(1024) void k_scan_excl(int64_t n, const int64_t* __restrict__ in,
-                                                    OUT* __restrict__ out,
-                                                    int64_t* __restrict__ scalars) {
-    constexpr int ITEMS = 8;
-    __shared__ long long wsum[16];
-    const int tid = threadIdx.x, l = lane_id(), w = tid >> 6;
-    long long carry = 0;
-    for (int64_t base = 0; base < n; base += 1024 * ITEMS) {
-        long long v[ITEMS];
-        long long tsum = 0;
-#pragma unroll
-        for (int j = 0; j < ITEMS; ++j) {
-            const int64_t idx = base + (int64_t)tid * ITEMS + j;
-            v[j] = idx < n ? in[idx] : 0;
-            tsum += v[j];
-        }
-        const long long incl = wave_incl_sum64(tsum);
-        if (l == WAVE - 1) wsum[w] = incl;
-        __syncthreads();
-        long long wbase = 0, btot = 0;
-        for (int q = 0; q < 16; ++q) {
-            const long long x = wsum[q];
-            if (q < w) wbase += x;
-            btot += x;
-        }
-        long long run = carry + wbase + incl - tsum;
-#pragma unroll
-        for (int j = 0; j < ITEMS; ++j) {
-            const int64_t idx = base + (int64_t)tid * ITEMS + j;
-            if (idx < n) out[idx] = (OUT)run;
-            run += v[j];
-        }
-        carry += btot;
-        __syncthreads();
-    }
-    if (tid == 0) {
-        out[n] = (OUT)carry;
-        scalars[0] = carry;
-        scalars[1] = (sizeof(OUT) == 4 && carry > 2147483647LL) ? 1 : 0;
-    }
-}
-
-// ---------------------------------------------------------------------------------------
-// Symbolic phase: structural nnz of each output row (no values).  One wave per row, a
-// private bitmap window in LDS.  Rows of C wider than one window walk B with cursors.
+// Symbolic phase (general path): structural nnz of each output row (no values).  One wave
+// per row, a private bitmap window in LDS.  Rows of C wider than one window walk B with
+// cursors.  Rows come either from the range [row0, row0 + nrows) or, when `list` is not
+// null, from list[0 .. *list_count) (rows the short-row kernel spilled); waves loop over
+// their share of rows.
 template <typename IP>
 __global__ __launch_bounds__(BLOCK) void k_symbolic(
     int64_t row0, int64_t nrows, int64_t ncols, const IP* __restrict__ Ap,
     const int32_t* __restrict__ Aj, const IP* __restrict__ Bp, const int32_t* __restrict__ Bj,
-    int64_t* __restrict__ row_cnt, uint32_t* __restrict__ cur, int64_t nz0) {
+    int64_t* __restrict__ row_cnt, uint32_t* __restrict__ cur, int64_t nz0,
+    const int32_t* __restrict__ list, const int32_t* __restrict__ list_count) {
     __shared__ uint32_t lds[WPB][SymGeom::BYTES / 4];
     const int l = lane_id();
     const int wv = threadIdx.x >> 6;
-    const int64_t row = row0 + (int64_t)blockIdx.x * WPB + wv;
-    if (row >= row0 + nrows) return;
     uint32_t* bits = lds[wv];
     int* marker = (int*)(bits + SymGeom::NWMAX);
-    const int64_t a0 = Ap[row], a1 = Ap[row + 1];
-    long long total = 0;
-    if (a0 < a1 && ncols > 0) {
-        const bool single = ncols <= 32LL * SymGeom::NWMAX;
-        for (int64_t lo = 0; lo < ncols;) {
-            const int64_t hi = single ? ncols : min(ncols, lo + 32LL * SymGeom::NWMAX);
-            const int nw = (int)((hi - lo + 31) >> 5);
-            for (int w = l; w < nw; w += WAVE) bits[w] = 0u;
-            wsync();
-            for (int64_t b = a0; b < a1; b += WAVE) {
-                const int64_t jj = b + l;
-                if (single) {
-                    long long beg = 0;
-                    int cnt = 0;
-                    if (jj < a1) {
+    const int64_t count = list ? (int64_t)*list_count : nrows;
+    for (int64_t it = (int64_t)blockIdx.x * WPB + wv; it < count; it += (int64_t)gridDim.x * WPB) {
+        const int64_t row = list ? (int64_t)list[it] : row0 + it;
+        const int64_t a0 = Ap[row], a1 = Ap[row + 1];
+        long long total = 0;
+        if (a0 < a1 && ncols > 0) {
+            const bool single = ncols <= 32LL * SymGeom::NWMAX;
+            for (int64_t lo = 0; lo < ncols;) {
+                const int64_t hi = single ? ncols : min(ncols, lo + 32LL * SymGeom::NWMAX);
+                const int nw = (int)((hi - lo + 31) >> 5);
+                for (int w = l; w < nw; w += WAVE) bits[w] = 0u;
+                wsync();
+                for (int64_t b = a0; b < a1; b += WAVE) {
+                    const int64_t jj = b + l;
+                    if (single) {
+                        long long beg = 0;
+                        int cnt = 0;
+                        if (jj < a1) {
+                            const int32_t k = Aj[jj];
+                            beg = Bp[k];
+                            cnt = (int)(Bp[k + 1] - beg);
+                        }
+                        for_each_product(beg, cnt, marker, [&](bool v, int, long long idx) {
+                            if (v) set_bit(bits, Bj[idx]);
+                        });
+                    } else if (jj < a1) {
                         const int32_t k = Aj[jj];
-                        beg = Bp[k];
-                        cnt = (int)(Bp[k + 1] - beg);
-                    }
-                    for_each_product(beg, cnt, marker, [&](bool v, int, long long idx) {
-                        if (v) set_bit(bits, Bj[idx]);
-                    });
-                } else if (jj < a1) {
-                    const int32_t k = Aj[jj];
-                    const int64_t rb = Bp[k], re = Bp[k + 1];
-                    int64_t p = rb + (lo == 0 ? 0 : (int64_t)cur[jj - nz0]);
-                    while (p < re) {
-                        int c[4];
+                        const int64_t rb = Bp[k], re = Bp[k + 1];
+                        int64_t p = rb + (lo == 0 ? 0 : (int64_t)cur[jj - nz0]);
+                        while (p < re) {
+                            int c[4];
 #pragma unroll
-                        for (int u = 0; u < 4; ++u) c[u] = (p + u < re) ? Bj[p + u] : 0x7fffffff;
-                        int n = 0;
+                            for (int u = 0; u < 4; ++u) c[u] = (p + u < re) ? Bj[p + u] : 0x7fffffff;
+                            int n = 0;
 #pragma unroll
-                        for (int u = 0; u < 4; ++u)
-                            if (c[u] < hi) { set_bit(bits, (int)(c[u] - lo)); ++n; }
-                        p += n;
-                        if (n < 4) break;
+                            for (int u = 0; u < 4; ++u)
+                                if (c[u] < hi) { set_bit(bits, (int)(c[u] - lo)); ++n; }
+                            p += n;
+                            if (n < 4) break;
+                        }
+                        cur[jj - nz0] = (uint32_t)(p - rb);
                     }
-                    cur[jj - nz0] = (uint32_t)(p - rb);
                 }
+                wsync();
+                long long cnt = 0;
+                for (int w = l; w < nw; w += WAVE) cnt += __popc(bits[w]);
+                total += wave_sum64(cnt);
+                wsync();
+                lo = hi;
             }
-            wsync();
-            long long cnt = 0;
-            for (int w = l; w < nw; w += WAVE) cnt += __popc(bits[w]);
-            total += wave_sum64(cnt);
-            wsync();
-            lo = hi;
         }
+        if (l == 0) row_cnt[row] = total;
     }
-    if (l == 0) row_cnt[row] = total;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -152,13 +112,15 @@ __global__ __launch_bounds__(BLOCK) void k_numeric(
     const int32_t* __restrict__ Aj, const T* __restrict__ Ax, const IP* __restrict__ Bp,
     const int32_t* __restrict__ Bj, const T* __restrict__ Bx, const OFF* __restrict__ Coff,
     int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha, int64_t* __restrict__ row_cnt,
-    uint32_t* __restrict__ seg, int64_t nz0, int64_t seg_len) {
+    uint32_t* __restrict__ seg, int64_t nz0, int64_t seg_len, const int32_t* __restrict__ list,
+    const int32_t* __restrict__ list_count) {
     using G = NumGeom<T>;
     __shared__ __attribute__((aligned(16))) char lds_raw[WPB][G::BYTES];
     const int l = lane_id();
     const int wv = threadIdx.x >> 6;
-    const int64_t row = row0 + (int64_t)blockIdx.x * WPB + wv;
-    if (row >= row0 + nrows) return;
+    const int64_t count = list ? (int64_t)*list_count : nrows;
+    for (int64_t it = (int64_t)blockIdx.x * WPB + wv; it < count; it += (int64_t)gridDim.x * WPB) {
+    const int64_t row = list ? (int64_t)list[it] : row0 + it;
     char* base = lds_raw[wv];
     T* acc = (T*)base;
     uint32_t* bits = (uint32_t*)(base + sizeof(T) * G::CAP);
@@ -274,7 +236,8 @@ __global__ __launch_bounds__(BLOCK) void k_numeric(
                         const uint32_t key = (seq << 6) | (uint32_t)l;
                         if (pending) atomicMin(&tag[pos], key);
                         wsync();
-                        if (pending && tag[pos] == key) {
+                        if (pending && __hip_atomic_load(&tag[pos], __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_WAVEFRONT) == key) {
                             acc[pos] = add_rn(acc[pos], prod);
                             pending = false;
                         }
@@ -306,6 +269,375 @@ __global__ __launch_bounds__(BLOCK) void k_numeric(
         }
     }
     if (UB && l == 0) row_cnt[row] = written;
+    }  // rows of this wave
+}
+
+// ---------------------------------------------------------------------------------------
+// Short-row kernel: one wave per output row whose A row has <= 64 entries, whose product
+// count is <= PLONG, whose structural nnz is <= CAP and whose columns fit one 16384-column
+// bitmap (the shape of BASELINE config 2).  Products are enumerated in flattened (jj, kk)
+// order, 64 per step: a step's lanes find their A entry with a marker write + DPP max
+// scan, so every product of the row is fetched with independent loads (one memory round
+// trip when the row has <= 512 products: they stay in registers between the structure
+// and the value pass; longer rows re-read B for the value pass).  The bitmap is kept as 8
+// contiguous words per lane (b128 LDS access), its popcount prefix gives each column its
+// output position, values are added in (jj, kk) order with lowest-lane-first owner rounds,
+// and each lane writes its own run of the (already sorted) output.
+// MODE: SHORT_SYM counts nnz per row (ALG2/3 symbolic), SHORT_NUM writes at C's exact row
+// pointer, SHORT_NUMUB writes at an upper-bound offset and records nnz (ALG1).  Rows outside
+// the limits are appended to `spill` (handled by the next kernel; the list order does not
+// affect any result).  Rows come from [row0, row0 + nrows) or, with `list`, from
+// list[0 .. *list_count).
+enum { SHORT_SYM = 0, SHORT_NUM = 1, SHORT_NUMUB = 2 };
+
+template <int CAP_, int PLONG_, int WPB_, int R_> struct ShortCfg {
+    static constexpr int R = R_;               // register-resident products per lane
+    static constexpr int PREG = R * WAVE;      // 512: rows up to this keep products in VGPRs
+    static constexpr int PLONG = PLONG_;       // longest product list taken
+    static constexpr int CAP = CAP_;           // most output entries per row
+    static constexpr int NW = 512;             // bitmap words: <= 16384 columns
+    static constexpr int WPB = WPB_;           // waves per block
+};
+using ShortSmall = ShortCfg<512, 4096, 4, 8>;      // ~10 KB LDS per wave: 16 waves / CU
+using ShortMedium = ShortCfg<2048, 65536, 2, 16>;  // tail rows of the same shape (~27 KB/wave,
+                                                   // 1024 products in registers)
+
+template <typename T, typename IP, typename G, bool VALS> struct ShortLds {
+    uint32_t bits[G::NW];
+    uint16_t wpre[G::NW];
+    T acc[VALS ? G::CAP + 1 : 1];              // + a dummy slot; marker bytes in pass 1
+    uint32_t tag[VALS ? G::CAP + 1 : 1];
+    int8_t mk[VALS ? 1 : G::PREG + 16];        // symbolic mode: its own marker bytes
+    T ja[WAVE];
+    IP jb0[WAVE];
+    uint16_t joff[WAVE];
+    int8_t marker[WAVE + 4];                   // + a dummy byte
+};
+
+// Lane -> A-entry map for the 64 products starting at c0: lanes whose segment starts in
+// [c0, c0+64) drop their lane id at that offset, a DPP max-scan (seeded with the carry of
+// the previous chunk) fills the gaps.  Branch-free: lanes with nothing to mark write the
+// dummy byte.  Returns the A entry (lane) of product c0 + lane; updates `carry`.
+template <typename L>
+__device__ __forceinline__ int chunk_src(L& S, int l, int cnt, int off, int c0, int& carry) {
+    S.marker[l] = -1;
+    wsync();
+    if (cnt > 0 && off >= c0 && off < c0 + WAVE) S.marker[off - c0] = (int8_t)l;
+    wsync();
+    const int src = max(wave_incl_max_dpp((int)S.marker[l]), carry);
+    carry = readlane_i(src, WAVE - 1);
+    return src;
+}
+
+template <typename T, typename IP, typename OFF, int MODE, typename G>
+__global__ __launch_bounds__(G::WPB * WAVE) void k_short(
+    int64_t row0, int64_t nrows, int64_t ncols, const IP* __restrict__ Ap,
+    const int32_t* __restrict__ Aj, const T* __restrict__ Ax, const IP* __restrict__ Bp,
+    const int32_t* __restrict__ Bj, const T* __restrict__ Bx, const OFF* __restrict__ Coff,
+    int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha, int64_t* __restrict__ row_cnt,
+    int32_t* __restrict__ spill, int32_t* __restrict__ spill_count,
+    const int32_t* __restrict__ list, const int32_t* __restrict__ list_count) {
+    constexpr int R = G::R;
+    constexpr bool VALS = MODE != SHORT_SYM;
+    __shared__ __attribute__((aligned(16))) ShortLds<T, IP, G, VALS> lds[G::WPB];
+    const int l = lane_id();
+    const int wv = uniform((int)(threadIdx.x >> 6));
+    ShortLds<T, IP, G, VALS>& S = lds[wv];
+    const int64_t count = list ? (int64_t)*list_count : nrows;
+    for (int64_t it = (int64_t)blockIdx.x * G::WPB + wv; it < count; it += (int64_t)gridDim.x * G::WPB) {
+        const int64_t row = list ? (int64_t)uniform(list[it]) : row0 + it;
+        const int64_t a0 = Ap[row];
+        const int nA = (int)(Ap[row + 1] - a0);
+        if (nA <= 0 || ncols <= 0) {
+            if (MODE != SHORT_NUM && l == 0) row_cnt[row] = 0;
+            continue;
+        }
+        if (nA > WAVE || ncols > 32LL * G::NW) {
+            if (l == 0) spill[atomicAdd(spill_count, 1)] = (int32_t)row;
+            continue;
+        }
+        int cnt = 0;
+        IP b0 = 0;
+        T av = (T)0;
+        if (l < nA) {
+            const int32_t k = Aj[a0 + l];
+            b0 = Bp[k];
+            cnt = (int)(Bp[k + 1] - b0);
+            if (VALS) av = Ax[a0 + l];
+        }
+        const int incl = wave_incl_sum_dpp(cnt);
+        const int off = incl - cnt;
+        const int P = readlane_i(incl, WAVE - 1);
+        if (P > G::PLONG) {
+            if (l == 0) spill[atomicAdd(spill_count, 1)] = (int32_t)row;
+            continue;
+        }
+        if (P == 0) {
+            if (MODE != SHORT_NUM && l == 0) row_cnt[row] = 0;
+            continue;
+        }
+        S.jb0[l] = b0;
+        S.joff[l] = (uint16_t)off;
+        if (VALS) S.ja[l] = av;
+        uint4* bits4 = reinterpret_cast<uint4*>(S.bits);
+        bits4[2 * l] = make_uint4(0u, 0u, 0u, 0u);
+        bits4[2 * l + 1] = make_uint4(0u, 0u, 0u, 0u);
+        wsync();
+        const int nch = (P + WAVE - 1) / WAVE;
+        const bool inreg = P <= G::PREG;
+        int col[R];
+        T prd[R];
+        int carry = -1;
+        // ---- pass 1: structure; for short lists the products stay in registers
+        if (inreg) {
+            // lane -> A-entry map of every chunk at once: each A entry drops its lane id at
+            // the first product it owns, a DPP max-scan per chunk (carried across chunks)
+            // fills the gaps.  The marker bytes borrow the accumulator area.
+            int8_t* mk = VALS ? reinterpret_cast<int8_t*>(S.acc) : S.mk;
+            static_assert(G::PREG % (WAVE * 8) == 0, "marker init assumes 8-byte pieces");
+#pragma unroll
+            for (int q = 0; q < G::PREG / (WAVE * 8); ++q)
+                reinterpret_cast<uint64_t*>(mk)[q * WAVE + l] = ~0ull;
+            wsync();
+            if (cnt > 0) mk[off] = (int8_t)l;
+            wsync();
+            int mrk[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) mrk[r] = r < nch ? (int)mk[r * WAVE + l] : -1;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                col[r] = -1;
+                prd[r] = (T)0;
+                if (r < nch) {
+                    const int src = max(wave_incl_max_dpp(mrk[r]), carry);
+                    carry = readlane_i(src, WAVE - 1);
+                    const int t = r * WAVE + l;
+                    const bool v = t < P;
+                    const IP idx = v ? S.jb0[src] + (IP)(t - (int)S.joff[src]) : (IP)0;
+                    const int c = Bj[idx];
+                    if (VALS) prd[r] = mul_rn(S.ja[src], Bx[idx]);
+                    col[r] = v ? c : -1;
+                    if (v) set_bit(S.bits, c);
+                }
+            }
+        } else {
+            for (int c0 = 0; c0 < P; c0 += WAVE) {
+                const int src = chunk_src(S, l, cnt, off, c0, carry);
+                const int t = c0 + l;
+                const bool v = t < P;
+                const IP idx = v ? S.jb0[src] + (IP)(t - (int)S.joff[src]) : (IP)0;
+                const int c = Bj[idx];
+                if (v) set_bit(S.bits, c);
+            }
+        }
+        wsync();
+        // ---- popcount prefix over this lane's 8 contiguous words
+        const uint4 q0 = bits4[2 * l], q1 = bits4[2 * l + 1];
+        const int c0 = __popc(q0.x), c1 = __popc(q0.y), c2 = __popc(q0.z), c3 = __popc(q0.w);
+        const int c4 = __popc(q1.x), c5 = __popc(q1.y), c6 = __popc(q1.z), c7 = __popc(q1.w);
+        const int mine = c0 + c1 + c2 + c3 + c4 + c5 + c6 + c7;
+        const int pincl = wave_incl_sum_dpp(mine);
+        const int nnz = readlane_i(pincl, WAVE - 1);
+        if (nnz > G::CAP) {
+            if (l == 0) spill[atomicAdd(spill_count, 1)] = (int32_t)row;
+            continue;
+        }
+        if (MODE == SHORT_SYM) {
+            if (l == 0) row_cnt[row] = nnz;
+            continue;
+        }
+        const int p0 = pincl - mine;
+        {
+            const int p1 = p0 + c0, p2 = p1 + c1, p3 = p2 + c2, p4 = p3 + c3, p5 = p4 + c4,
+                      p6 = p5 + c5, p7 = p6 + c6;
+            uint4 w;
+            w.x = (uint32_t)p0 | ((uint32_t)p1 << 16);
+            w.y = (uint32_t)p2 | ((uint32_t)p3 << 16);
+            w.z = (uint32_t)p4 | ((uint32_t)p5 << 16);
+            w.w = (uint32_t)p6 | ((uint32_t)p7 << 16);
+            reinterpret_cast<uint4*>(S.wpre)[l] = w;
+        }
+        for (int p = l; p < nnz; p += WAVE) {
+            S.acc[p] = (T)0;
+            S.tag[p] = 0xffffffffu;
+        }
+        wsync();
+        // ---- pass 2: values in (jj, kk) order; equal columns of one step go lowest lane
+        // first (ds_min on an owner tag).  Branch-free: losers and inactive lanes address
+        // the dummy slot.
+        uint32_t seq = 0x3ffffffu;
+        auto accumulate = [&](int c, T pv) -> int {
+            int pos = G::CAP;
+            if (c >= 0) {
+                const int w = c >> 5;
+                pos = (int)S.wpre[w] + __popc(S.bits[w] & ((1u << (c & 31)) - 1u));
+            }
+            bool pending = c >= 0;
+            // (no fences inside: the atomic and the atomic load of one address keep their
+            // order, and LDS operations of a wave execute in issue order)
+            while (__ballot(pending)) {
+                const uint32_t key = (seq << 6) | (uint32_t)l;
+                if (pending) {
+                    atomicMin(&S.tag[pos], key);
+                    if (__hip_atomic_load(&S.tag[pos], __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_WAVEFRONT) == key) {
+                        S.acc[pos] = add_rn(S.acc[pos], pv);
+                        pending = false;
+                    }
+                }
+                --seq;
+            }
+            return pos;
+        };
+        if (inreg) {
+            int pos[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                pos[r] = G::CAP;
+                if (r < nch) pos[r] = accumulate(col[r], prd[r]);
+            }
+            wsync();
+            // column list straight from the registers (equal columns write equal values)
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (r < nch) S.tag[pos[r]] = (uint32_t)col[r];
+        } else {
+            carry = -1;
+            for (int cc0 = 0; cc0 < P; cc0 += WAVE) {
+                const int src = chunk_src(S, l, cnt, off, cc0, carry);
+                const int t = cc0 + l;
+                const bool v = t < P;
+                const IP idx = v ? S.jb0[src] + (IP)(t - (int)S.joff[src]) : (IP)0;
+                const int c = Bj[idx];
+                const T pv = mul_rn(S.ja[src], Bx[idx]);
+                accumulate(v ? c : -1, pv);
+                if (seq < 4096u) {   // re-arm the tag space (very long rows only)
+                    wsync();
+                    for (int p = l; p < nnz; p += WAVE) S.tag[p] = 0xffffffffu;
+                    seq = 0x3ffffffu;
+                    wsync();
+                }
+            }
+            wsync();
+            // column list from this lane's 8 bitmap words
+            uint64_t m0 = (uint64_t)q0.x | ((uint64_t)q0.y << 32);
+            uint64_t m1 = (uint64_t)q0.z | ((uint64_t)q0.w << 32);
+            uint64_t m2 = (uint64_t)q1.x | ((uint64_t)q1.y << 32);
+            uint64_t m3 = (uint64_t)q1.z | ((uint64_t)q1.w << 32);
+            const int cbase = 256 * l;
+            int p = p0;
+            while (m0 | m1 | m2 | m3) {
+                int cc;
+                if (m0) { cc = cbase + __builtin_ctzll(m0); m0 &= m0 - 1; }
+                else if (m1) { cc = cbase + 64 + __builtin_ctzll(m1); m1 &= m1 - 1; }
+                else if (m2) { cc = cbase + 128 + __builtin_ctzll(m2); m2 &= m2 - 1; }
+                else { cc = cbase + 192 + __builtin_ctzll(m3); m3 &= m3 - 1; }
+                S.tag[p++] = (uint32_t)cc;
+            }
+        }
+        wsync();
+        {
+            int32_t* __restrict__ crow = Cj + (int64_t)Coff[row];
+            T* __restrict__ xrow = Cx + (int64_t)Coff[row];
+            for (int p = l; p < nnz; p += WAVE) {
+                crow[p] = (int32_t)S.tag[p];
+                const T val = S.acc[p];
+                xrow[p] = (alpha == (T)1) ? val : mul_rn(alpha, val);
+            }
+        }
+        if (MODE == SHORT_NUMUB && l == 0) row_cnt[row] = nnz;
+        wsync();
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Single-pass exclusive scan with decoupled look-back.  out[0..n) = exclusive prefix of
+// in[], out[n] = total, scalars[0] = total, scalars[1] = 1 if the total overflows OUT.
+// `status` holds 1 ticket word + one 8-byte status per tile and must be zero on entry.
+// Status word: bits 63..62 = 0 not ready / 1 tile aggregate / 2 inclusive prefix,
+// bits 61..0 = value.  Tiles take tickets in order, so every tile a block waits on has
+// started; the status word is its own payload (8-byte agent-scope atomics on both sides,
+// MI355X_MICROARCH.md, "Valid forms").
+constexpr int SCAN_ITEMS = 8;
+constexpr int SCAN_TILE = BLOCK * SCAN_ITEMS;   // 2048
+
+template <typename OUT>
+__global__ __launch_bounds__(BLOCK) void k_scan_lb(int64_t n, const int64_t* __restrict__ in,
+                                                   OUT* __restrict__ out,
+                                                   unsigned long long* __restrict__ status,
+                                                   int64_t* __restrict__ scalars) {
+    constexpr unsigned long long VMASK = (1ull << 62) - 1;
+    __shared__ long long wsum[WPB];
+    __shared__ long long prefix_s;
+    __shared__ int bid_s;
+    const int tid = threadIdx.x, l = lane_id(), wv = tid >> 6;
+    if (tid == 0) bid_s = (int)atomicAdd(&status[0], 1ull);
+    __syncthreads();
+    const int64_t bid = bid_s;
+    const int64_t base = bid * SCAN_TILE + (int64_t)tid * SCAN_ITEMS;
+    long long v[SCAN_ITEMS];
+    long long tsum = 0;
+#pragma unroll
+    for (int j = 0; j < SCAN_ITEMS; ++j) {
+        v[j] = base + j < n ? in[base + j] : 0;
+        tsum += v[j];
+    }
+    const long long incl = wave_incl_sum64(tsum);
+    if (l == WAVE - 1) wsum[wv] = incl;
+    __syncthreads();
+    long long wbase = 0, btot = 0;
+#pragma unroll
+    for (int q = 0; q < WPB; ++q) {
+        if (q < wv) wbase += wsum[q];
+        btot += wsum[q];
+    }
+    unsigned long long* st = status + 1;
+    if (wv == 0) {
+        long long prefix = 0;
+        if (bid == 0) {
+            if (l == 0)
+                __hip_atomic_store(&st[0], (2ull << 62) | (unsigned long long)btot, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            if (l == 0)
+                __hip_atomic_store(&st[bid], (1ull << 62) | (unsigned long long)btot, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            int64_t j = bid - 1;
+            for (;;) {
+                const int64_t q = j - l;
+                unsigned long long s = 0;
+                if (q >= 0) {
+                    do {
+                        s = __hip_atomic_load(&st[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    } while ((s >> 62) == 0);
+                }
+                const unsigned long long incm = __ballot(q >= 0 && (s >> 62) == 2);
+                const int stop = incm ? __ffsll((long long)incm) - 1 : WAVE;
+                const long long val = (q >= 0 && l <= stop) ? (long long)(s & VMASK) : 0;
+                prefix += wave_sum64(val);
+                if (incm || j - WAVE < 0) break;
+                j -= WAVE;
+            }
+            if (l == 0)
+                __hip_atomic_store(&st[bid], (2ull << 62) | (unsigned long long)(prefix + btot),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (l == 0) prefix_s = prefix;
+    }
+    __syncthreads();
+    long long run = prefix_s + wbase + incl - tsum;
+#pragma unroll
+    for (int j = 0; j < SCAN_ITEMS; ++j) {
+        if (base + j < n) out[base + j] = (OUT)run;
+        run += v[j];
+    }
+    const int64_t ntiles = n > 0 ? (n + SCAN_TILE - 1) / SCAN_TILE : 1;
+    if (bid == ntiles - 1 && tid == 0) {
+        const long long total = prefix_s + btot;
+        out[n] = (OUT)total;
+        scalars[0] = total;
+        scalars[1] = (sizeof(OUT) == 4 && total > 2147483647LL) ? 1 : 0;
+    }
 }
 
 // ---------------------------------------------------------------------------------------

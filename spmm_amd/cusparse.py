@@ -47,17 +47,23 @@ class SpgemmStats:
 last_stats = SpgemmStats()
 
 
+_available = None
+
+
 def check_availability(name: str) -> bool:
-    """True when the named routine can run here (a gfx950 device and the built library)."""
+    """True when the named routine can run here (a gfx950 device and the built library).
+    Memoized like the reference's ``@_util.memoize()`` check (cusparse.py:169-186)."""
+    global _available
     if name not in ("spgemm", "validate_csr"):
         raise ValueError(f"No available version information specified for {name}")
-    try:
-        if not torch.cuda.is_available():
-            return False
-        _lib.get_handle(torch.cuda.current_device())
-        return True
-    except Exception:
-        return False
+    if _available is None:
+        try:
+            _available = bool(torch.cuda.is_available())
+            if _available:
+                _lib.get_handle(torch.cuda.current_device())
+        except Exception:
+            _available = False
+    return _available
 
 
 def _csr_view(m: csr_matrix) -> SpgCsr:
@@ -157,9 +163,9 @@ def spgemm(a, b, alpha=1, alg=0, chunk_fraction=0.2, verbose=False):
         nnzc = int(nnz.value)
         indices = torch.empty(nnzc, dtype=torch.int32, device=dev)
         data = torch.empty(nnzc, dtype=a.data.dtype, device=dev)
-        c = csr_matrix((data, indices, indptr), shape=(m, n), canonical=True)
-        c.indptr = indptr   # keep the int32/int64 choice made above
-        vc = _csr_view(c)
+        c = csr_matrix._from_parts(data, indices, indptr, (m, n), canonical=True)
+        vc = SpgCsr(m, n, nnzc, indptr.data_ptr(), indices.data_ptr() if nnzc else 0,
+                    data.data_ptr() if nnzc else 0, _IT[indptr.dtype], _VT[data.dtype])
         ctype = ctypes.c_double if a.data.dtype == torch.float64 else ctypes.c_float
         al = ctype(float(alpha))
         check(lib.spg_numeric(h.ptr, plan, ctypes.byref(al), ctypes.byref(vc)), "spg_numeric")

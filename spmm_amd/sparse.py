@@ -123,6 +123,15 @@ class csr_matrix(_SparseBase):
         if self.indptr.numel() != self._shape[0] + 1:
             raise ValueError("indptr length must be rows + 1")
 
+    @classmethod
+    def _from_parts(cls, data, indices, indptr, shape, canonical=True):
+        """Wrap device tensors as-is (no conversion, no copy) -- the shim's result path."""
+        self = cls.__new__(cls)
+        self.data, self.indices, self.indptr = data, indices, indptr
+        self._shape = (int(shape[0]), int(shape[1]))
+        self._canonical = canonical
+        return self
+
     # ------------------------------------------------------------------ structure
     @property
     def has_canonical_format(self) -> bool:
