@@ -61,6 +61,7 @@ struct spg_plan_s {
     int32_t* spill = nullptr;       // rows the short-row kernel hands to the general kernel
     unsigned long long* scan_status = nullptr;   // look-back scan: ticket + one word per tile
     bool use_short = false;         // dispatch the short-row kernel first
+    unsigned list_grid = 16;        // blocks of the general kernel that takes its spills
     int symbolic_runs = 0;          // spg_symbolic may be called again (e.g. int32 -> int64)
     std::vector<int64_t> chunk_rows;   // ALG3 row boundaries (chunk c = [r[c], r[c+1]))
     std::vector<int64_t> chunk_nz;     // A entry offset of each boundary
@@ -323,7 +324,6 @@ spg_status_t run_symbolic_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_
     if (p.use_short) {
         int32_t* cnt = spill_counts(p, false);
         int32_t* l1 = p.spill;
-        int32_t* l2 = p.spill + p.A.rows;
         hipLaunchKernelGGL((k_short<double, IP, int64_t, SHORT_SYM, ShortSmall>),
                            dim3((unsigned)grid_for(n, ShortSmall::WPB)), dim3(ShortSmall::WPB * WAVE), 0,
                            h->stream, r0, n, p.B.cols, Ap, Aj, (const double*)nullptr, Bp, Bj,
@@ -331,15 +331,9 @@ spg_status_t run_symbolic_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_
                            (double*)nullptr, 1.0, p.row_cnt, l1, cnt, (const int32_t*)nullptr,
                            (const int32_t*)nullptr);
         SPG_LAUNCHED(h);
-        hipLaunchKernelGGL((k_short<double, IP, int64_t, SHORT_SYM, ShortMedium>), dim3(list_grid(std::min<int64_t>(n, 256))),
-                           dim3(ShortMedium::WPB * WAVE), 0, h->stream, r0, n, p.B.cols, Ap, Aj,
-                           (const double*)nullptr, Bp, Bj, (const double*)nullptr, (const int64_t*)nullptr,
-                           (int32_t*)nullptr, (double*)nullptr, 1.0, p.row_cnt, l2, cnt + 1,
-                           (const int32_t*)l1, (const int32_t*)cnt);
-        SPG_LAUNCHED(h);
-        hipLaunchKernelGGL(k_symbolic<IP>, dim3(list_grid(std::min<int64_t>(n, 256))), dim3(BLOCK), 0, h->stream, r0, n,
-                           p.B.cols, Ap, Aj, Bp, Bj, p.row_cnt, p.seg, nz0, (const int32_t*)l2,
-                           (const int32_t*)(cnt + 1));
+        hipLaunchKernelGGL(k_symbolic<IP>, dim3(p.list_grid), dim3(BLOCK), 0, h->stream, r0, n,
+                           p.B.cols, Ap, Aj, Bp, Bj, p.row_cnt, p.seg, nz0, (const int32_t*)l1,
+                           (const int32_t*)cnt);
     } else {
         hipLaunchKernelGGL(k_symbolic<IP>, dim3((unsigned)grid_for(n, WPB)), dim3(BLOCK), 0, h->stream,
                            r0, n, p.B.cols, Ap, Aj, Bp, Bj, p.row_cnt, p.seg, nz0,
@@ -365,20 +359,14 @@ spg_status_t run_numeric_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_t
     if (p.use_short) {
         int32_t* cnt = spill_counts(p, true);
         int32_t* l1 = p.spill;
-        int32_t* l2 = p.spill + p.A.rows;
         hipLaunchKernelGGL((k_short<T, IP, OFF, MODE, ShortSmall>), dim3((unsigned)grid_for(n, ShortSmall::WPB)),
                            dim3(ShortSmall::WPB * WAVE), 0, h->stream, r0, n, p.B.cols, Ap, Aj, Ax, Bp, Bj,
                            Bx, off, cj, cx, alpha, p.row_cnt, l1, cnt, (const int32_t*)nullptr,
                            (const int32_t*)nullptr);
         SPG_LAUNCHED(h);
-        hipLaunchKernelGGL((k_short<T, IP, OFF, MODE, ShortMedium>), dim3(list_grid(std::min<int64_t>(n, 256))),
-                           dim3(ShortMedium::WPB * WAVE), 0, h->stream, r0, n, p.B.cols, Ap, Aj, Ax, Bp,
-                           Bj, Bx, off, cj, cx, alpha, p.row_cnt, l2, cnt + 1, (const int32_t*)l1,
-                           (const int32_t*)cnt);
-        SPG_LAUNCHED(h);
-        hipLaunchKernelGGL((k_numeric<T, IP, OFF, UB>), dim3(list_grid(std::min<int64_t>(n, 256))), dim3(BLOCK), 0, h->stream,
+        hipLaunchKernelGGL((k_numeric<T, IP, OFF, UB>), dim3(p.list_grid), dim3(BLOCK), 0, h->stream,
                            r0, n, p.B.cols, Ap, Aj, Ax, Bp, Bj, Bx, off, cj, cx, alpha, p.row_cnt,
-                           p.seg, nz0, p.seg_len, (const int32_t*)l2, (const int32_t*)(cnt + 1));
+                           p.seg, nz0, p.seg_len, (const int32_t*)l1, (const int32_t*)cnt);
     } else {
         hipLaunchKernelGGL((k_numeric<T, IP, OFF, UB>), dim3((unsigned)grid_for(n, WPB)), dim3(BLOCK), 0,
                            h->stream, r0, n, p.B.cols, Ap, Aj, Ax, Bp, Bj, Bx, off, cj, cx, alpha,
@@ -554,6 +542,9 @@ spg_status_t spg_plan(spg_handle_t h, const spg_csr_t* A, const spg_csr_t* B, sp
     tmp.cf = chunk_fraction;
     tmp.seg_len = A->nnz;
     tmp.use_short = want_short(*A, *B);
+    // spills are rare for the shapes the short kernel is chosen for (A rows > 64 entries or
+    // C wider than 16384 columns): a small grid keeps the usually-empty launch cheap
+    tmp.list_grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(64, grid_for(A->rows, 1024)));
     // ALG1 and ALG3 size their buffers / chunks from the product counts, which needs the
     // device once.  The size query and the building call of one plan see the same
     // operands, so the building call reuses what the query measured.

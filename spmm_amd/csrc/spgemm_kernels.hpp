@@ -297,17 +297,17 @@ template <int CAP_, int PLONG_, int WPB_, int R_> struct ShortCfg {
     static constexpr int CAP = CAP_;           // most output entries per row
     static constexpr int NW = 512;             // bitmap words: <= 16384 columns
     static constexpr int WPB = WPB_;           // waves per block
+    static constexpr int MKB = (PREG + 511) / 512 * 512;   // marker bytes (8 per lane per piece)
 };
-using ShortSmall = ShortCfg<512, 4096, 4, 8>;      // ~10 KB LDS per wave: 16 waves / CU
-using ShortMedium = ShortCfg<2048, 65536, 2, 16>;  // tail rows of the same shape (~27 KB/wave,
-                                                   // 1024 products in registers)
+using ShortSmall = ShortCfg<512, 65535, 4, 8>;     // ~10 KB LDS per wave: 16 waves / CU;
+                                                   // 640 products per row in registers
 
 template <typename T, typename IP, typename G, bool VALS> struct ShortLds {
     uint32_t bits[G::NW];
     uint16_t wpre[G::NW];
     T acc[VALS ? G::CAP + 1 : 1];              // + a dummy slot; marker bytes in pass 1
     uint32_t tag[VALS ? G::CAP + 1 : 1];
-    int8_t mk[VALS ? 1 : G::PREG + 16];        // symbolic mode: its own marker bytes
+    int8_t mk[VALS ? 1 : G::MKB];              // symbolic mode: its own marker bytes
     T ja[WAVE];
     IP jb0[WAVE];
     uint16_t joff[WAVE];
@@ -394,9 +394,9 @@ __global__ __launch_bounds__(G::WPB * WAVE) void k_short(
             // the first product it owns, a DPP max-scan per chunk (carried across chunks)
             // fills the gaps.  The marker bytes borrow the accumulator area.
             int8_t* mk = VALS ? reinterpret_cast<int8_t*>(S.acc) : S.mk;
-            static_assert(G::PREG % (WAVE * 8) == 0, "marker init assumes 8-byte pieces");
+            static_assert(!VALS || G::MKB <= (int)sizeof(T) * G::CAP, "markers must fit acc");
 #pragma unroll
-            for (int q = 0; q < G::PREG / (WAVE * 8); ++q)
+            for (int q = 0; q < G::MKB / (WAVE * 8); ++q)
                 reinterpret_cast<uint64_t*>(mk)[q * WAVE + l] = ~0ull;
             wsync();
             if (cnt > 0) mk[off] = (int8_t)l;
@@ -438,10 +438,6 @@ __global__ __launch_bounds__(G::WPB * WAVE) void k_short(
         const int mine = c0 + c1 + c2 + c3 + c4 + c5 + c6 + c7;
         const int pincl = wave_incl_sum_dpp(mine);
         const int nnz = readlane_i(pincl, WAVE - 1);
-        if (nnz > G::CAP) {
-            if (l == 0) spill[atomicAdd(spill_count, 1)] = (int32_t)row;
-            continue;
-        }
         if (MODE == SHORT_SYM) {
             if (l == 0) row_cnt[row] = nnz;
             continue;
@@ -457,20 +453,15 @@ __global__ __launch_bounds__(G::WPB * WAVE) void k_short(
             w.w = (uint32_t)p6 | ((uint32_t)p7 << 16);
             reinterpret_cast<uint4*>(S.wpre)[l] = w;
         }
-        for (int p = l; p < nnz; p += WAVE) {
-            S.acc[p] = (T)0;
-            S.tag[p] = 0xffffffffu;
-        }
-        wsync();
         // ---- pass 2: values in (jj, kk) order; equal columns of one step go lowest lane
-        // first (ds_min on an owner tag).  Branch-free: losers and inactive lanes address
-        // the dummy slot.
+        // first (ds_min on an owner tag).  `wb` is the first output position of the column
+        // window being accumulated (0 for rows that fit CAP).
         uint32_t seq = 0x3ffffffu;
-        auto accumulate = [&](int c, T pv) -> int {
+        auto accumulate = [&](int c, T pv, int wb) -> int {
             int pos = G::CAP;
             if (c >= 0) {
                 const int w = c >> 5;
-                pos = (int)S.wpre[w] + __popc(S.bits[w] & ((1u << (c & 31)) - 1u));
+                pos = (int)S.wpre[w] + __popc(S.bits[w] & ((1u << (c & 31)) - 1u)) - wb;
             }
             bool pending = c >= 0;
             // (no fences inside: the atomic and the atomic load of one address keep their
@@ -489,61 +480,83 @@ __global__ __launch_bounds__(G::WPB * WAVE) void k_short(
             }
             return pos;
         };
-        if (inreg) {
-            int pos[R];
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                pos[r] = G::CAP;
-                if (r < nch) pos[r] = accumulate(col[r], prd[r]);
+        // Column windows made of whole lanes' 8-word groups (<= 256 entries each, so a
+        // window always advances), each holding <= CAP entries; rows with nnz <= CAP are one
+        // window.  Register-resident products are filtered per window; longer rows re-read
+        // the window's products from B (L2-resident by now).
+        for (int L0 = 0; L0 < WAVE;) {
+            int L1 = WAVE, wb = 0, wn = nnz;
+            if (nnz > G::CAP) {
+                wb = readlane_i(p0, L0);
+                L1 = (int)__popcll(__ballot(pincl <= wb + G::CAP));
+                if (L1 <= L0) L1 = L0 + 1;
+                wn = (L1 < WAVE ? readlane_i(p0, L1) : nnz) - wb;
+            }
+            const int clo = 256 * L0, chi = 256 * L1;
+            for (int p = l; p < wn; p += WAVE) {
+                S.acc[p] = (T)0;
+                S.tag[p] = 0xffffffffu;
             }
             wsync();
-            // column list straight from the registers (equal columns write equal values)
+            seq = 0x3ffffffu;
+            if (inreg) {
+                int pos[R];
 #pragma unroll
-            for (int r = 0; r < R; ++r)
-                if (r < nch) S.tag[pos[r]] = (uint32_t)col[r];
-        } else {
-            carry = -1;
-            for (int cc0 = 0; cc0 < P; cc0 += WAVE) {
-                const int src = chunk_src(S, l, cnt, off, cc0, carry);
-                const int t = cc0 + l;
-                const bool v = t < P;
-                const IP idx = v ? S.jb0[src] + (IP)(t - (int)S.joff[src]) : (IP)0;
-                const int c = Bj[idx];
-                const T pv = mul_rn(S.ja[src], Bx[idx]);
-                accumulate(v ? c : -1, pv);
-                if (seq < 4096u) {   // re-arm the tag space (very long rows only)
-                    wsync();
-                    for (int p = l; p < nnz; p += WAVE) S.tag[p] = 0xffffffffu;
-                    seq = 0x3ffffffu;
-                    wsync();
+                for (int r = 0; r < R; ++r) {
+                    pos[r] = G::CAP;
+                    if (r < nch)
+                        pos[r] = accumulate(col[r] >= clo && col[r] < chi ? col[r] : -1, prd[r], wb);
+                }
+                wsync();
+                // column list straight from the registers (equal columns write equal values)
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+                    if (r < nch && pos[r] < G::CAP) S.tag[pos[r]] = (uint32_t)col[r];
+            } else {
+                carry = -1;
+                for (int cc0 = 0; cc0 < P; cc0 += WAVE) {
+                    const int src = chunk_src(S, l, cnt, off, cc0, carry);
+                    const int t = cc0 + l;
+                    const bool v = t < P;
+                    const IP idx = v ? S.jb0[src] + (IP)(t - (int)S.joff[src]) : (IP)0;
+                    const int c = Bj[idx];
+                    const T pv = mul_rn(S.ja[src], Bx[idx]);
+                    accumulate(v && c >= clo && c < chi ? c : -1, pv, wb);
+                    if (seq < 4096u) {   // re-arm the tag space (very long rows only)
+                        wsync();
+                        for (int p = l; p < wn; p += WAVE) S.tag[p] = 0xffffffffu;
+                        seq = 0x3ffffffu;
+                        wsync();
+                    }
+                }
+                wsync();
+                if (l >= L0 && l < L1) {   // column list from this lane's 8 bitmap words
+                    uint64_t m0 = (uint64_t)q0.x | ((uint64_t)q0.y << 32);
+                    uint64_t m1 = (uint64_t)q0.z | ((uint64_t)q0.w << 32);
+                    uint64_t m2 = (uint64_t)q1.x | ((uint64_t)q1.y << 32);
+                    uint64_t m3 = (uint64_t)q1.z | ((uint64_t)q1.w << 32);
+                    const int cbase = 256 * l;
+                    int p = p0 - wb;
+                    while (m0 | m1 | m2 | m3) {
+                        int cc;
+                        if (m0) { cc = cbase + __builtin_ctzll(m0); m0 &= m0 - 1; }
+                        else if (m1) { cc = cbase + 64 + __builtin_ctzll(m1); m1 &= m1 - 1; }
+                        else if (m2) { cc = cbase + 128 + __builtin_ctzll(m2); m2 &= m2 - 1; }
+                        else { cc = cbase + 192 + __builtin_ctzll(m3); m3 &= m3 - 1; }
+                        S.tag[p++] = (uint32_t)cc;
+                    }
                 }
             }
             wsync();
-            // column list from this lane's 8 bitmap words
-            uint64_t m0 = (uint64_t)q0.x | ((uint64_t)q0.y << 32);
-            uint64_t m1 = (uint64_t)q0.z | ((uint64_t)q0.w << 32);
-            uint64_t m2 = (uint64_t)q1.x | ((uint64_t)q1.y << 32);
-            uint64_t m3 = (uint64_t)q1.z | ((uint64_t)q1.w << 32);
-            const int cbase = 256 * l;
-            int p = p0;
-            while (m0 | m1 | m2 | m3) {
-                int cc;
-                if (m0) { cc = cbase + __builtin_ctzll(m0); m0 &= m0 - 1; }
-                else if (m1) { cc = cbase + 64 + __builtin_ctzll(m1); m1 &= m1 - 1; }
-                else if (m2) { cc = cbase + 128 + __builtin_ctzll(m2); m2 &= m2 - 1; }
-                else { cc = cbase + 192 + __builtin_ctzll(m3); m3 &= m3 - 1; }
-                S.tag[p++] = (uint32_t)cc;
-            }
-        }
-        wsync();
-        {
-            int32_t* __restrict__ crow = Cj + (int64_t)Coff[row];
-            T* __restrict__ xrow = Cx + (int64_t)Coff[row];
-            for (int p = l; p < nnz; p += WAVE) {
+            int32_t* __restrict__ crow = Cj + (int64_t)Coff[row] + wb;
+            T* __restrict__ xrow = Cx + (int64_t)Coff[row] + wb;
+            for (int p = l; p < wn; p += WAVE) {
                 crow[p] = (int32_t)S.tag[p];
                 const T val = S.acc[p];
                 xrow[p] = (alpha == (T)1) ? val : mul_rn(alpha, val);
             }
+            wsync();
+            L0 = L1;
         }
         if (MODE == SHORT_NUMUB && l == 0) row_cnt[row] = nnz;
         wsync();

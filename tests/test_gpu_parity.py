@@ -233,3 +233,22 @@ def test_validate_csr():
     bad = csr_matrix((np.ones(2), np.array([0, 9], np.int32), np.array([0, 1, 2])),
                      shape=(2, 4), device=_dev())
     assert cusparse.validate_csr(bad) == -1
+
+
+def test_short_kernel_long_rows():
+    """Rows the short-row kernel keeps but cannot hold in registers: more than 512 products
+    with more than 512 output entries (in-kernel column windows) and with heavy column
+    overlap (many products per output entry)."""
+    rng = np.random.default_rng(21)
+    cases = [
+        (sp.random(200, 2000, density=0.02, format="csr", random_state=rng),
+         sp.random(2000, 8000, density=0.005, format="csr", random_state=rng)),   # P~1600, nnz~1450
+        (sp.random(150, 2000, density=0.03, format="csr", random_state=rng),
+         sp.random(2000, 300, density=0.05, format="csr", random_state=rng)),    # P~900, nnz<=300
+        (sp.random(100, 3000, density=0.02, format="csr", random_state=rng),
+         sp.random(3000, 16384, density=0.01, format="csr", random_state=rng)),  # widest short case
+    ]
+    for A, B in cases:
+        A.sort_indices(); B.sort_indices()
+        for alg in (1, 2, 3):
+            _assert_same(_gpu(A, B, alg=alg), oracle.spgemm(A, B, keep_zeros=True, sort=True))
