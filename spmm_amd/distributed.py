@@ -82,3 +82,15 @@ def spgemm_rowblock(A_block: csr_matrix, B: csr_matrix, alg: int = 0, chunk_frac
     """This rank's C slab = A_block . B (row block r0:r1 of the global C)."""
     from . import cusparse
     return cusparse.spgemm(A_block, B, alg=alg, chunk_fraction=chunk_fraction)
+
+
+def stitch_indptr(slab_indptrs, slab_nnz):
+    """Global row pointer from per-rank slab row pointers (host numpy, int64): slab r's
+    pointers shifted by the nnz of slabs 0..r-1 (the offsets allgather_nnz provides)."""
+    out = [np.zeros(1, np.int64)]
+    base = 0
+    for p, nz in zip(slab_indptrs, slab_nnz):
+        p = np.asarray(p, dtype=np.int64)
+        out.append(p[1:] + base)
+        base += int(nz)
+    return np.concatenate(out)

@@ -1,0 +1,80 @@
+"""The reference's script-level checks, run through the ports (GPU): the cupy_cusparse
+text-file parity pipeline (Python shim vs native driver, bitwise), the determinism check,
+the ALG comparison profiler, the sparse-vs-dense harness and the row-block runner."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+H = os.path.join(ROOT, "harness")
+
+
+def run(cmd, env=None, timeout=600):
+    e = dict(os.environ)
+    e.update(env or {})
+    r = subprocess.run(cmd, capture_output=True, text=True, env=e, timeout=timeout, cwd=ROOT)
+    return r
+
+
+@pytest.mark.parametrize("alg", [1, 2, 3])
+def test_cupy_cusparse_pipeline(tmp_path, alg):
+    r = run(["bash", os.path.join(H, "cupy_cusparse", f"run_all_alg{alg}.sh"), str(tmp_path / "dump")],
+            env={"SIZES": "32 64 256", "DENSITIES": "0.01 0.1 0.5"})
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "9 PASS / 0 FAIL / 9 TOTAL" in r.stdout
+
+
+def test_native_driver_fp64(tmp_path):
+    """SPG_DTYPE=float64 driver path against the Python shim (fp64 text, %.17g)."""
+    import numpy as np
+    import scipy.sparse as sp
+    sys.path.insert(0, ROOT)
+    from oracle import oracle
+    from spmm_amd.txtio import load_csr_txt, save_csr_txt
+    A = sp.random(300, 300, density=0.05, format="csr", random_state=2)
+    B = sp.random(300, 300, density=0.05, format="csr", random_state=3)
+    A.sort_indices(); B.sort_indices()
+    save_csr_txt(str(tmp_path / "A"), A.indptr, A.indices, A.data)
+    save_csr_txt(str(tmp_path / "B"), B.indptr, B.indices, B.data)
+    exe = os.path.join(ROOT, "drivers", "bin", "spgemm_from_txt_alg2")
+    r = run([exe, str(tmp_path / "A"), str(tmp_path / "B"), str(tmp_path / "C")], env={"SPG_DTYPE": "float64"})
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.startswith("[C++] ALG2 wrote")
+    _, _, p, j, x = load_csr_txt(str(tmp_path / "C"), np.float64)
+    rp, rj, rx = oracle.spgemm(A, B, keep_zeros=True, sort=True)
+    assert np.array_equal(p, rp) and np.array_equal(j, rj)
+    assert np.array_equal(x.view(np.uint64), rx.view(np.uint64))
+
+
+def test_deterministic_script():
+    r = run(["bash", os.path.join(H, "deterministic", "test_deterministic.sh")], env={"SEEDS": "1"})
+    assert r.returncode == 0, r.stdout + r.stderr
+    for alg in (1, 2, 3):
+        assert f"alg{alg} is deterministic" in r.stdout
+
+
+def test_alg_comparison_profiler():
+    r = run([sys.executable, os.path.join(H, "SpGEMM_alg_comparison", "profiler.py"),
+             "--size", "512", "--density", "0.1", "--runs", "3"])
+    assert r.returncode == 0, r.stderr
+    for alg in (1, 2, 3):
+        assert f"(alg={alg})" in r.stdout
+
+
+def test_dense_vs_sparse_harness():
+    r = run([sys.executable, os.path.join(H, "dense_vs_sparseGEMM", "main.py"), "--size", "1024",
+             "--density", "0.01", "--runs", "2", "--dtype", "float64"])
+    assert r.returncode == 0, r.stderr
+    assert "[sparse, inputs_on_gpu]" in r.stdout and "[dense, inputs_on_gpu]" in r.stdout
+
+
+def test_rowblock_runner_single_gpu():
+    r = run([sys.executable, os.path.join(H, "multi_gpu", "spgemm_rowblock.py"), "--n", "65536",
+             "--density", "1e-3", "--steps", "1", "--warmup", "0", "--check", "8"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["sampled_rows_bad"] == 0 and line["nnzC"] > 0
