@@ -14,6 +14,7 @@
 
 #include "spgemm.h"
 #include "spgemm_kernels.hpp"
+#include "spgemm_tile.hpp"
 
 using namespace spg;
 
@@ -61,6 +62,16 @@ struct spg_plan_s {
     int32_t* spill = nullptr;       // rows the short-row kernel hands to the general kernel
     unsigned long long* scan_status = nullptr;   // look-back scan: ticket + one word per tile
     bool use_short = false;         // dispatch the short-row kernel first
+    bool use_tile = false;          // wide-row path: (row, column tile) items
+    int tws = 10;                   // log2 of the tile width
+    int G = 1;                      // tiles per row
+    int TR = 1;                     // tiles per wave task (a run of one row's tiles)
+    int twss = 10;                  // log2 of the symbolic tile width (>= tws, <= 16)
+    bool counts_ready = false;      // a symbolic pass has completed (counts / offsets valid)
+    uint32_t* tidx = nullptr;       // B column-tile index, B.rows * (G + 1)
+    uint32_t* bitmap = nullptr;     // per-item column bitmaps (symbolic -> numeric)
+    int64_t* item_cnt = nullptr;    // per-item counts, scanned in place into offsets
+    bool tidx_built = false;
     unsigned list_grid = 16;        // blocks of the general kernel that takes its spills
     int symbolic_runs = 0;          // spg_symbolic may be called again (e.g. int32 -> int64)
     std::vector<int64_t> chunk_rows;   // ALG3 row boundaries (chunk c = [r[c], r[c+1]))
@@ -88,9 +99,41 @@ inline bool want_short(const spg_csr_t& A, const spg_csr_t& B) {
     return avgA <= 48.0 && avgA * avgB <= 400.0;
 }
 
-// grid of a list-mode general kernel: enough waves to cover the spilled rows of a
-// launch over `rows` rows, capped (the waves loop over the list)
-inline unsigned list_grid(int64_t rows) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>(grid_for(rows, WPB), 1024)); }
+// Wide rows go to the tile path when their C rows are dense enough that a tile of up to
+// 4096 columns holds a useful number of entries.  The tile width keeps the expected
+// entries of a tile within TILE_CAP (or is at most TILE_CAP, which bounds them).
+inline bool want_tile(const spg_csr_t& A, const spg_csr_t& B, int& tws, int& G) {
+    if (A.rows == 0 || B.rows == 0 || B.cols == 0 || A.nnz == 0 || B.nnz == 0) return false;
+    const double avgA = (double)A.nnz / (double)A.rows;
+    const double avgB = (double)B.nnz / (double)B.rows;
+    const double frac = 1.0 - std::exp(-avgA * avgB / (double)B.cols);   // expected C row density
+    tws = 8;
+    for (int t = 8; t <= 12; ++t) {
+        const double tw = (double)(1 << t);
+        if (tw <= TILE_CAP || frac * tw <= 0.95 * TILE_CAP) tws = t;
+        if (tw >= (double)B.cols) break;
+    }
+    if (frac * (double)(1 << tws) < 64.0) return false;
+    G = (int)((B.cols + (1 << tws) - 1) >> tws);
+    return (double)A.rows * G < 2.0e9;
+}
+
+// grid of a tile kernel over `tasks` wave tasks: a multiple of 8 (XCD-aware block ids)
+inline unsigned tile_grid(int64_t tasks) {
+    const int64_t nb = std::max<int64_t>(1, std::min<int64_t>(grid_for(tasks, TILE_WPB), 1 << 22));
+    return (unsigned)((nb + 7) / 8 * 8);
+}
+
+// symbolic tile: the narrowest width >= the numeric tile whose B segments (expected B row
+// entries per tile) reach 64 entries -- long coalesced reads -- capped at 65536 columns
+// and at the (pow2-rounded) row width
+inline int sym_tile_log2(const spg_csr_t& B, int tws) {
+    const double avgB = B.rows > 0 ? (double)B.nnz / (double)B.rows : 0.0;
+    int t = tws;
+    while (t < 16 && ((int64_t)1 << t) < B.cols && avgB * (double)((int64_t)1 << t) / (double)B.cols < 64.0) ++t;
+    return t;
+}
+
 
 spg_status_t hip_fail(spg_handle_t h, hipError_t e) {
     if (h) h->last_hip = (int)e;
@@ -224,18 +267,34 @@ spg_status_t read_scalars(spg_handle_t h, const int64_t* dev, int n, int64_t* ou
 }
 
 struct Layout {
-    size_t scalars = 0, row_cnt = 0, seg = 0, spill = 0, status = 0, ub = 0, tj = 0, tx = 0, total = 0;
+    size_t scalars = 0, row_cnt = 0, seg = 0, spill = 0, status = 0, ub = 0, tj = 0, tx = 0;
+    size_t tidx = 0, items = 0, bitmap = 0, total = 0;
 };
+
+inline int64_t tile_items(const spg_plan_s& p) { return p.use_tile ? p.A.rows * p.G : 0; }
+
+// status words: products scan | row-pointer scan | item scan (tile path)
+inline size_t status_words(const spg_plan_s& p) {
+    return 2 * (size_t)(scan_tiles(p.A.rows) + 1) + (p.use_tile ? (size_t)scan_tiles(tile_items(p)) + 1 : 0);
+}
+inline unsigned long long* item_scan_status(const spg_plan_s& p) {
+    return p.scan_status + 2 * (scan_tiles(p.A.rows) + 1);
+}
 
 Layout make_layout(const spg_plan_s& p) {
     Layout L;
     size_t off = 0;
     L.scalars = off; off = align_up(off + 16 * sizeof(int64_t));
-    L.status = off;  off = align_up(off + sizeof(unsigned long long) * 2 * (size_t)(scan_tiles(p.A.rows) + 1));
+    L.status = off;  off = align_up(off + sizeof(unsigned long long) * status_words(p));
     L.row_cnt = off; off = align_up(off + sizeof(int64_t) * (size_t)(p.A.rows + 1));
     L.seg = off;     off = align_up(off + sizeof(uint32_t) * 2 * (size_t)std::max<int64_t>(p.seg_len, 1));
     L.spill = off;   off = align_up(off + sizeof(int32_t) * 2 * (size_t)std::max<int64_t>(p.A.rows, 1));
-    if (p.alg == SPG_ALG1) {
+    if (p.use_tile) {
+        L.tidx = off;  off = align_up(off + sizeof(uint32_t) * (size_t)p.B.rows * (size_t)(p.G + 1));
+        L.items = off; off = align_up(off + sizeof(int64_t) * (size_t)(tile_items(p) + 1));
+        L.bitmap = off; off = align_up(off + sizeof(uint32_t) * (size_t)tile_items(p) * (size_t)((1 << p.tws) >> 5));
+    }
+    if (p.alg == SPG_ALG1 && !p.use_tile) {
         L.ub = off; off = align_up(off + sizeof(int64_t) * (size_t)(p.A.rows + 1));
         L.tj = off; off = align_up(off + sizeof(int32_t) * (size_t)std::max<int64_t>(p.P, 1));
         L.tx = off; off = align_up(off + vbytes(p.A.value_type) * (size_t)std::max<int64_t>(p.P, 1));
@@ -250,7 +309,12 @@ void carve(spg_plan_s& p, const Layout& L) {
     p.seg = (uint32_t*)(p.ws + L.seg);
     p.spill = (int32_t*)(p.ws + L.spill);
     p.scan_status = (unsigned long long*)(p.ws + L.status);
-    if (p.alg == SPG_ALG1) {
+    if (p.use_tile) {
+        p.tidx = (uint32_t*)(p.ws + L.tidx);
+        p.item_cnt = (int64_t*)(p.ws + L.items);
+        p.bitmap = (uint32_t*)(p.ws + L.bitmap);
+    }
+    if (p.alg == SPG_ALG1 && !p.use_tile) {
         p.ub = (int64_t*)(p.ws + L.ub);
         p.tj = (int32_t*)(p.ws + L.tj);
         p.tx = (void*)(p.ws + L.tx);
@@ -321,7 +385,18 @@ spg_status_t run_symbolic_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_
     const int32_t* Aj = (const int32_t*)p.A.indices;
     const int32_t* Bj = (const int32_t*)p.B.indices;
     PhaseTimer pt(h, SPG_PHASE_SYMBOLIC);
-    if (p.use_short) {
+    if (p.use_tile) {
+        if (!p.tidx_built) {
+            hipLaunchKernelGGL(k_tile_index<IP>, dim3((unsigned)grid_for(p.B.rows, 4)), dim3(256), 0,
+                               h->stream, p.B.rows, Bp, Bj, p.tws, p.G, p.tidx);
+            SPG_LAUNCHED(h);
+            p.tidx_built = true;
+        }
+        const int R = 1 << (p.twss - p.tws);
+        hipLaunchKernelGGL(k_tile_sym<IP>, dim3(tile_grid(n * ((p.G + R - 1) / R))), dim3(TILE_WPB * WAVE), 0,
+                           h->stream, r0, n, p.tws, p.G, p.twss, Ap, Aj, Bp, Bj, (const uint32_t*)p.tidx,
+                           p.bitmap, p.item_cnt);
+    } else if (p.use_short) {
         int32_t* cnt = spill_counts(p, false);
         int32_t* l1 = p.spill;
         hipLaunchKernelGGL((k_short<double, IP, int64_t, SHORT_SYM, ShortSmall>),
@@ -356,7 +431,12 @@ spg_status_t run_numeric_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_t
     const T* Bx = (const T*)p.B.values;
     constexpr int MODE = UB ? SHORT_NUMUB : SHORT_NUM;
     PhaseTimer pt(h, SPG_PHASE_NUMERIC);
-    if (p.use_short) {
+    if (p.use_tile) {
+        hipLaunchKernelGGL((k_tile<T, IP, SHORT_NUM, false>), dim3(tile_grid(n * p.G)), dim3(TILE_WPB * WAVE),
+                           0, h->stream, r0, n, p.B.cols, p.tws, p.G, p.TR, Ap, Aj, Ax, Bp, Bj, Bx,
+                           (const uint32_t*)p.tidx, p.bitmap, (int64_t*)nullptr, (const int64_t*)p.item_cnt, cj,
+                           cx, alpha);
+    } else if (p.use_short) {
         int32_t* cnt = spill_counts(p, true);
         int32_t* l1 = p.spill;
         hipLaunchKernelGGL((k_short<T, IP, OFF, MODE, ShortSmall>), dim3((unsigned)grid_for(n, ShortSmall::WPB)),
@@ -379,6 +459,21 @@ spg_status_t run_numeric_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_t
 
 template <typename OUT>
 spg_status_t run_scan(spg_handle_t h, spg_plan_s& p, void* out) {
+    if (p.use_tile) {
+        // item counts -> item offsets in place (once: a repeated spg_symbolic reuses them);
+        // C's row pointer = the offset of each row's first item (overflow of an int32 row
+        // pointer is checked on the host)
+        if (!p.counts_ready) {
+            spg_status_t st = launch_scan<int64_t>(h, tile_items(p), (const int64_t*)p.item_cnt, p.item_cnt,
+                                                   item_scan_status(p), p.scalars, false);
+            if (st) return st;
+        }
+        PhaseTimer pt(h, SPG_PHASE_SCAN);
+        hipLaunchKernelGGL(k_items_to_rowptr<OUT>, dim3((unsigned)grid_for(p.A.rows + 1, 256)), dim3(256), 0,
+                           h->stream, p.A.rows, p.G, (const int64_t*)p.item_cnt, (OUT*)out);
+        SPG_LAUNCHED(h);
+        return SPG_STATUS_SUCCESS;
+    }
     // the row-pointer scan uses the second status region of the control block
     return launch_scan<OUT>(h, p.A.rows, (const int64_t*)p.row_cnt, (OUT*)out,
                             p.scan_status + scan_tiles(p.A.rows) + 1, p.scalars, false);
@@ -409,7 +504,7 @@ spg_status_t alg1_compute(spg_handle_t h, spg_plan_s& p) {
 template <typename T, typename IP, typename IPC>
 spg_status_t numeric_typed(spg_handle_t h, spg_plan_s& p, const spg_csr_t& C, T alpha) {
     const IPC* cp = (const IPC*)C.indptr;
-    if (p.alg == SPG_ALG1) {
+    if (p.alg == SPG_ALG1 && !p.use_tile) {
         if (p.A.rows > 0) {
             PhaseTimer pt(h, SPG_PHASE_COMPACT);
             hipLaunchKernelGGL((k_compact<T, IPC>), dim3((unsigned)grid_for(p.A.rows, WPB)), dim3(BLOCK), 0,
@@ -542,6 +637,11 @@ spg_status_t spg_plan(spg_handle_t h, const spg_csr_t* A, const spg_csr_t* B, sp
     tmp.cf = chunk_fraction;
     tmp.seg_len = A->nnz;
     tmp.use_short = want_short(*A, *B);
+    tmp.use_tile = !tmp.use_short && want_tile(*A, *B, tmp.tws, tmp.G);
+    if (tmp.use_tile) {
+        tmp.TR = 1;
+        tmp.twss = sym_tile_log2(*B, tmp.tws);
+    }
     // spills are rare for the shapes the short kernel is chosen for (A rows > 64 entries or
     // C wider than 16384 columns): a small grid keeps the usually-empty launch cheap
     tmp.list_grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(64, grid_for(A->rows, 1024)));
@@ -551,7 +651,7 @@ spg_status_t spg_plan(spg_handle_t h, const spg_csr_t* A, const spg_csr_t* B, sp
     const bool same_as_query = h->q_valid && h->q_alg == tmp.alg && h->q_cf == chunk_fraction &&
                                std::memcmp(&h->q_A, A, sizeof(spg_csr_t)) == 0 &&
                                std::memcmp(&h->q_B, B, sizeof(spg_csr_t)) == 0;
-    if (tmp.alg == SPG_ALG1) {
+    if (tmp.alg == SPG_ALG1 && !tmp.use_tile) {
         if (workspace && same_as_query) {
             tmp.P = h->q_P;
         } else {
@@ -570,6 +670,7 @@ spg_status_t spg_plan(spg_handle_t h, const spg_csr_t* A, const spg_csr_t* B, sp
             return st;
         }
     }
+    if (tmp.use_tile) tmp.seg_len = 1;   // no cursor scratch on the tile path
     if (!workspace) {
         h->q_valid = true;
         h->q_A = *A;
@@ -597,7 +698,7 @@ spg_status_t spg_plan(spg_handle_t h, const spg_csr_t* A, const spg_csr_t* B, sp
         hipError_t e1 = hipMemsetAsync(p->ws, 0, L.row_cnt, h->stream);   // scalars + status
         if (e1 != hipSuccess) { delete p; return hip_fail(h, e1); }
     }
-    if (p->alg == SPG_ALG1) {
+    if (p->alg == SPG_ALG1 && !p->use_tile) {
         // upper-bound offsets for the single pass: product prefix straight into the workspace
         spg_status_t st2 = products_prefix(h, p->A, p->B, p->row_cnt, p->ub, p->scalars + 2,
                                            p->scan_status, false);
@@ -630,28 +731,31 @@ spg_status_t spg_symbolic(spg_handle_t h, spg_plan_t p, void* C_indptr, spg_inde
     SPG_HIP(h, hipSetDevice(h->device));
     spg_status_t st;
     const bool i64 = p->A.indptr_type == SPG_INDEX_64I;
-    if (p->symbolic_runs++ > 0) {
-        // a repeated call (e.g. retrying with int64 row pointers): re-arm the spill counters
-        // and the row-pointer scan's status words
+    if (p->symbolic_runs++ > 0 && !p->use_tile) {
+        // a repeated call (e.g. retrying with int64 row pointers): the row counts are kept;
+        // re-arm the row-pointer scan's status words
         const int64_t tiles = scan_tiles(p->A.rows) + 1;
-        SPG_HIP(h, hipMemsetAsync(p->scalars + 4, 0, 2 * sizeof(int64_t), h->stream));
         SPG_HIP(h, hipMemsetAsync(p->scan_status + tiles, 0, sizeof(unsigned long long) * tiles, h->stream));
     }
-    if (p->alg == SPG_ALG1) {
-        if (p->A.value_type == SPG_R_64F)
-            st = i64 ? alg1_compute<double, int64_t>(h, *p) : alg1_compute<double, int32_t>(h, *p);
-        else
-            st = i64 ? alg1_compute<float, int64_t>(h, *p) : alg1_compute<float, int32_t>(h, *p);
-    } else {
-        st = i64 ? symbolic_typed<int64_t>(h, *p) : symbolic_typed<int32_t>(h, *p);
+    if (!p->counts_ready) {
+        if (p->alg == SPG_ALG1 && !p->use_tile) {
+            if (p->A.value_type == SPG_R_64F)
+                st = i64 ? alg1_compute<double, int64_t>(h, *p) : alg1_compute<double, int32_t>(h, *p);
+            else
+                st = i64 ? alg1_compute<float, int64_t>(h, *p) : alg1_compute<float, int32_t>(h, *p);
+        } else {
+            st = i64 ? symbolic_typed<int64_t>(h, *p) : symbolic_typed<int32_t>(h, *p);
+        }
+        if (st) return st;
     }
-    if (st) return st;
     st = C_indptr_type == SPG_INDEX_64I ? run_scan<int64_t>(h, *p, C_indptr)
                                         : run_scan<int32_t>(h, *p, C_indptr);
     if (st) return st;
     int64_t sc[2];
     if ((st = read_scalars(h, p->scalars, 2, sc))) return st;
-    if (sc[1]) return SPG_STATUS_OVERFLOW;
+    p->counts_ready = true;      // counts (and tile offsets) stay valid for a repeated call
+    if (sc[1] || (p->use_tile && C_indptr_type == SPG_INDEX_32I && sc[0] > 2147483647LL))
+        return SPG_STATUS_OVERFLOW;
     p->nnzC = sc[0];
     p->c_indptr = C_indptr;
     p->c_indptr_type = C_indptr_type;

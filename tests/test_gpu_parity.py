@@ -252,3 +252,53 @@ def test_short_kernel_long_rows():
         A.sort_indices(); B.sort_indices()
         for alg in (1, 2, 3):
             _assert_same(_gpu(A, B, alg=alg), oracle.spgemm(A, B, keep_zeros=True, sort=True))
+
+
+def _skewed(rng, rows, k, n, dense_rows, base_density, b_density, dtype=np.float64):
+    """A: sparse rows plus a few full rows and some empty ones; B: uniform random."""
+    A = sp.random(rows, k, density=base_density, format="lil", random_state=rng, dtype=dtype)
+    for r in dense_rows:
+        A[r, :] = rng.standard_normal(k).astype(dtype)
+    for r in range(3, rows, 37):
+        A[r, :] = 0
+    A = sp.csr_matrix(A)
+    B = sp.random(k, n, density=b_density, format="csr", random_state=rng, dtype=dtype)
+    for M in (A, B):
+        M.sum_duplicates()
+        M.sort_indices()
+    return A, B
+
+
+def test_tile_path_windows_and_skew():
+    """Wide-row (row, column tile) path: 4096-column tiles whose dense rows need several
+    LDS windows per tile, empty A rows, a ragged last tile (n % 4096 != 0), alpha != 1,
+    every algorithm (ALG3 with many chunks)."""
+    rng = np.random.default_rng(31)
+    A, B = _skewed(rng, 384, 4096, 100003, dense_rows=[0, 17, 200, 383], base_density=0.05,
+                   b_density=0.001)
+    ref = oracle.spgemm(A, B, alpha=-0.75, keep_zeros=True, sort=True)
+    assert np.diff(ref[0]).max() > 4 * 1024        # some tiles hold several windows
+    for alg, cf in [(1, 0.2), (2, 0.2), (3, 0.2), (3, 0.02)]:
+        _assert_same(_gpu(A, B, alg=alg, alpha=-0.75, cf=cf), ref)
+
+
+def test_tile_path_dense_tiles_fp32_int64():
+    """1024-column tiles over a dense C (batches of 64 A entries with > 1024 products per
+    batch and tile), fp32 values, int64 row pointers, B with empty rows."""
+    from spmm_amd import cusparse
+    from spmm_amd.sparse import csr_matrix
+    rng = np.random.default_rng(32)
+    A = sp.random(300, 2500, density=0.2, format="csr", random_state=rng, dtype=np.float32)
+    B = sp.random(2500, 5000, density=0.25, format="lil", random_state=rng, dtype=np.float32)
+    B[10:40, :] = 0
+    B = sp.csr_matrix(B)
+    for M in (A, B):
+        M.sort_indices()
+    ref = oracle.spgemm(A, B, keep_zeros=True, sort=True)
+    dA, dB = csr_matrix(A, device=_dev()), csr_matrix(B, device=_dev())
+    dA.indptr = dA.indptr.to(torch.int64)
+    dB.indptr = dB.indptr.to(torch.int64)
+    for alg in (1, 2, 3):
+        C = cusparse.spgemm(dA, dB, alg=alg, chunk_fraction=0.1)
+        _assert_same((C.indptr.cpu().numpy().astype(np.int64), C.indices.cpu().numpy(),
+                      C.data.cpu().numpy()), ref)
