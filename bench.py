@@ -13,7 +13,7 @@ plan, symbolic with its nnz(C) host sync, C allocation, numeric), inputs residen
   the step), every rank computes its C slab; no collective inside the step.
   value = sum over ranks of 2*P_r per step / max-over-ranks step time.
 
-Also reported: ``roofline`` for the dominant kernel (k_numeric; algorithmic bytes per
+Also reported: ``roofline`` for the numeric-phase kernel (k_short here; algorithmic bytes per
 launch / its average device time from HIP events on the library's stream, SURVEY 8d
 compulsory-bytes model) and ``cpu_baseline`` (the oracle's C restatement of scipy's
 csr_matmat, single thread, on the same A and B, rank 0 at N=1), plus scipy itself.
@@ -141,6 +141,10 @@ def main():
     phases = h.get_timing()
     h.set_timing(False)
     dom = max(phases.items(), key=lambda kv: kv[1][0])
+    avgA, avgB = A.nnz / max(A.shape[0], 1), B.nnz / max(B.shape[0], 1)
+    # which kernel the numeric phase launches (the library's own dispatch rule, want_short)
+    num_kernel = ("k_short" if B.shape[1] <= 16384 and avgA <= 48 and avgA * avgB <= 400
+                  else "k_tile / k_numeric")
     dom_name, (dom_ms, dom_launches) = dom
     num_ms, num_launches = phases["numeric"]
     avg_num_ms = num_ms / max(num_launches, 1)
@@ -203,7 +207,7 @@ def main():
             "peak_hbm_bytes": int(peak_max),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "kernel": "k_numeric",
+                         "traffic": traffic, "kernel": num_kernel + " (numeric phase, one launch)",
                          "bytes_per_launch": int(bytes_launch),
                          "avg_launch_ms": round(avg_num_ms, 5)},
             "phases_ms_per_step": {k: round(v[0] / reps, 5) for k, v in phases.items() if v[1]},

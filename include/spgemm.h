@@ -160,6 +160,13 @@ spg_status_t spg_symbolic(spg_handle_t handle, spg_plan_t plan, void *C_indptr,
 spg_status_t spg_numeric(spg_handle_t handle, spg_plan_t plan, const void *alpha,
                          spg_csr_t *C);
 
+/* ALG1 single pass: after spg_symbolic, C's column indices and values may already sit
+ * compact in the workspace (nnzC entries at *indices / *values; NULL otherwise).  A
+ * caller may hand exactly these pointers to spg_numeric as C->indices / C->values: the
+ * numeric call then only scales by alpha in place (once) instead of copying.  No
+ * cuSPARSE counterpart; ignoring it keeps the cuSPARSE call sequence (a copy). */
+spg_status_t spg_result_in_workspace(spg_plan_t plan, void **indices, void **values);
+
 /* Bytes this multiply needs on the device beyond its inputs: workspace + C's three arrays
  * (the "peak HBM bytes" metric; inputs excluded like the reference's inputs-on-GPU
  * ΔPeak, dense_vs_sparseGEMM/utils.py:243-250).  Exact once spg_symbolic has run; before
@@ -186,11 +193,14 @@ spg_status_t spg_plan_destroy(spg_plan_t plan);
  * device.  Off by default (events cost a few microseconds per launch). */
 typedef enum {
     SPG_PHASE_PRODUCTS = 0,   /* k_row_products: P_i per row                      */
-    SPG_PHASE_SCAN = 1,       /* k_scan_excl: row pointer / product prefix          */
-    SPG_PHASE_SYMBOLIC = 2,   /* k_symbolic: structural nnz per row                 */
-    SPG_PHASE_NUMERIC = 3,    /* k_numeric: values (and ALG1 structure)             */
+    SPG_PHASE_SCAN = 1,       /* k_scan_lb / k_items_to_rowptr: prefix sums       */
+    SPG_PHASE_SYMBOLIC = 2,   /* k_short (count) / k_tile_sym / k_symbolic        */
+    SPG_PHASE_NUMERIC = 3,    /* k_short / k_tile / k_numeric: values (ALG1 also  */
+                              /* structure); one kernel per launch                */
     SPG_PHASE_COMPACT = 4,    /* k_compact: ALG1 copy into C                        */
     SPG_PHASE_VALIDATE = 5,   /* k_validate                                         */
+    SPG_PHASE_SPILL = 6,      /* k_symbolic / k_numeric over the rows the short-row */
+                              /* kernel handed on (list mode); k_tile_index         */
     SPG_NUM_PHASES = 8
 } spg_phase_t;
 

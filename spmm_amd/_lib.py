@@ -41,9 +41,9 @@ STATUS_OVERFLOW = 100
 EXPORTS = ("spg_version", "spg_status_string", "spg_create", "spg_destroy", "spg_set_stream",
            "spg_last_hip_error", "spg_plan", "spg_num_products", "spg_symbolic",
            "spg_numeric", "spg_peak_bytes", "spg_validate_csr", "spg_plan_destroy",
-           "spg_set_timing", "spg_get_timing")
+           "spg_set_timing", "spg_get_timing", "spg_result_in_workspace")
 
-PHASES = ("products", "scan", "symbolic", "numeric", "compact", "validate")
+PHASES = ("products", "scan", "symbolic", "numeric", "compact", "validate", "spill")
 NUM_PHASES = 8
 
 

@@ -68,6 +68,10 @@ struct spg_plan_s {
     int TR = 1;                     // tiles per wave task (a run of one row's tiles)
     int twss = 10;                  // log2 of the symbolic tile width (>= tws, <= 16)
     bool counts_ready = false;      // a symbolic pass has completed (counts / offsets valid)
+    unsigned long long* lb = nullptr;   // ALG1 single pass: per-row look-back status words
+    bool alg1_fused = false;        // C's arrays were written compact into tj/tx by one pass
+    bool fused_failed = false;      // the single pass met a row it cannot take
+    bool scaled_in_place = false;   // spg_numeric scaled the workspace result by alpha
     uint32_t* tidx = nullptr;       // B column-tile index, B.rows * (G + 1)
     uint32_t* bitmap = nullptr;     // per-item column bitmaps (symbolic -> numeric)
     int64_t* item_cnt = nullptr;    // per-item counts, scanned in place into offsets
@@ -240,6 +244,28 @@ spg_status_t products_prefix(spg_handle_t h, const spg_csr_t& A, const spg_csr_t
                                           : launch_products<int32_t>(h, A, B, cnt, pref, scal, status, zero_status);
 }
 
+spg_status_t read_scalars(spg_handle_t h, const int64_t* dev, int n, int64_t* out);
+
+// P alone (no per-row prefix): one flat pass over A's entries into handle scratch
+spg_status_t products_total(spg_handle_t h, const spg_csr_t& A, const spg_csr_t& B, int64_t* P) {
+    spg_status_t st = ensure_scratch(h, 256);
+    if (st) return st;
+    unsigned long long* acc = (unsigned long long*)h->scratch;
+    SPG_HIP(h, hipMemsetAsync(acc, 0, sizeof(unsigned long long), h->stream));
+    if (A.nnz > 0) {
+        PhaseTimer pt(h, SPG_PHASE_PRODUCTS);
+        const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(grid_for(A.nnz, BLOCK), 64));
+        if (A.indptr_type == SPG_INDEX_64I)
+            hipLaunchKernelGGL(k_products_total<int64_t>, dim3(grid), dim3(BLOCK), 0, h->stream, A.nnz,
+                               (const int32_t*)A.indices, (const int64_t*)B.indptr, acc);
+        else
+            hipLaunchKernelGGL(k_products_total<int32_t>, dim3(grid), dim3(BLOCK), 0, h->stream, A.nnz,
+                               (const int32_t*)A.indices, (const int32_t*)B.indptr, acc);
+        SPG_LAUNCHED(h);
+    }
+    return read_scalars(h, (const int64_t*)acc, 1, P);
+}
+
 // handle scratch for plan-time product prefixes: cnt[rows] | pref[rows+1] | scal[16] | status
 struct ScratchView {
     int64_t* cnt;
@@ -273,9 +299,13 @@ struct Layout {
 
 inline int64_t tile_items(const spg_plan_s& p) { return p.use_tile ? p.A.rows * p.G : 0; }
 
+// ALG1 runs as one fused pass (k_short SHORT_NUMLB) when the short-row kernel takes the shape
+inline bool fused_alg1(const spg_plan_s& p) { return p.alg == SPG_ALG1 && p.use_short && !p.use_tile; }
+
 // status words: products scan | row-pointer scan | item scan (tile path)
 inline size_t status_words(const spg_plan_s& p) {
-    return 2 * (size_t)(scan_tiles(p.A.rows) + 1) + (p.use_tile ? (size_t)scan_tiles(tile_items(p)) + 1 : 0);
+    return 2 * (size_t)(scan_tiles(p.A.rows) + 1) + (p.use_tile ? (size_t)scan_tiles(tile_items(p)) + 1 : 0) +
+           (fused_alg1(p) ? (size_t)grid_for(p.A.rows, ShortSmall::WPB) + 1 : 0);
 }
 inline unsigned long long* item_scan_status(const spg_plan_s& p) {
     return p.scan_status + 2 * (scan_tiles(p.A.rows) + 1);
@@ -309,6 +339,7 @@ void carve(spg_plan_s& p, const Layout& L) {
     p.seg = (uint32_t*)(p.ws + L.seg);
     p.spill = (int32_t*)(p.ws + L.spill);
     p.scan_status = (unsigned long long*)(p.ws + L.status);
+    if (fused_alg1(p)) p.lb = p.scan_status + 2 * (scan_tiles(p.A.rows) + 1);
     if (p.use_tile) {
         p.tidx = (uint32_t*)(p.ws + L.tidx);
         p.item_cnt = (int64_t*)(p.ws + L.items);
@@ -384,14 +415,15 @@ spg_status_t run_symbolic_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_
     const IP* Bp = (const IP*)p.B.indptr;
     const int32_t* Aj = (const int32_t*)p.A.indices;
     const int32_t* Bj = (const int32_t*)p.B.indices;
-    PhaseTimer pt(h, SPG_PHASE_SYMBOLIC);
     if (p.use_tile) {
         if (!p.tidx_built) {
+            PhaseTimer ps(h, SPG_PHASE_SPILL);
             hipLaunchKernelGGL(k_tile_index<IP>, dim3((unsigned)grid_for(p.B.rows, 4)), dim3(256), 0,
                                h->stream, p.B.rows, Bp, Bj, p.tws, p.G, p.tidx);
             SPG_LAUNCHED(h);
             p.tidx_built = true;
         }
+        PhaseTimer pt(h, SPG_PHASE_SYMBOLIC);
         const int R = 1 << (p.twss - p.tws);
         hipLaunchKernelGGL(k_tile_sym<IP>, dim3(tile_grid(n * ((p.G + R - 1) / R))), dim3(TILE_WPB * WAVE), 0,
                            h->stream, r0, n, p.tws, p.G, p.twss, Ap, Aj, Bp, Bj, (const uint32_t*)p.tidx,
@@ -399,17 +431,23 @@ spg_status_t run_symbolic_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_
     } else if (p.use_short) {
         int32_t* cnt = spill_counts(p, false);
         int32_t* l1 = p.spill;
-        hipLaunchKernelGGL((k_short<double, IP, int64_t, SHORT_SYM, ShortSmall>),
-                           dim3((unsigned)grid_for(n, ShortSmall::WPB)), dim3(ShortSmall::WPB * WAVE), 0,
-                           h->stream, r0, n, p.B.cols, Ap, Aj, (const double*)nullptr, Bp, Bj,
-                           (const double*)nullptr, (const int64_t*)nullptr, (int32_t*)nullptr,
-                           (double*)nullptr, 1.0, p.row_cnt, l1, cnt, (const int32_t*)nullptr,
-                           (const int32_t*)nullptr);
-        SPG_LAUNCHED(h);
+        {
+            PhaseTimer pt(h, SPG_PHASE_SYMBOLIC);
+            hipLaunchKernelGGL((k_short<double, IP, int64_t, SHORT_SYM, ShortSmall>),
+                               dim3((unsigned)grid_for(n, ShortSmall::WPB)), dim3(ShortSmall::WPB * WAVE), 0,
+                               h->stream, r0, n, p.B.cols, Ap, Aj, (const double*)nullptr, Bp, Bj,
+                               (const double*)nullptr, (const int64_t*)nullptr, (int32_t*)nullptr,
+                               (double*)nullptr, 1.0, p.row_cnt, l1, cnt, (const int32_t*)nullptr,
+                               (const int32_t*)nullptr, (unsigned long long*)nullptr, (int64_t*)nullptr,
+                               (int64_t*)nullptr);
+            SPG_LAUNCHED(h);
+        }
+        PhaseTimer ps(h, SPG_PHASE_SPILL);
         hipLaunchKernelGGL(k_symbolic<IP>, dim3(p.list_grid), dim3(BLOCK), 0, h->stream, r0, n,
                            p.B.cols, Ap, Aj, Bp, Bj, p.row_cnt, p.seg, nz0, (const int32_t*)l1,
                            (const int32_t*)cnt);
     } else {
+        PhaseTimer pt(h, SPG_PHASE_SYMBOLIC);
         hipLaunchKernelGGL(k_symbolic<IP>, dim3((unsigned)grid_for(n, WPB)), dim3(BLOCK), 0, h->stream,
                            r0, n, p.B.cols, Ap, Aj, Bp, Bj, p.row_cnt, p.seg, nz0,
                            (const int32_t*)nullptr, (const int32_t*)nullptr);
@@ -430,8 +468,8 @@ spg_status_t run_numeric_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_t
     const T* Ax = (const T*)p.A.values;
     const T* Bx = (const T*)p.B.values;
     constexpr int MODE = UB ? SHORT_NUMUB : SHORT_NUM;
-    PhaseTimer pt(h, SPG_PHASE_NUMERIC);
     if (p.use_tile) {
+        PhaseTimer pt(h, SPG_PHASE_NUMERIC);
         hipLaunchKernelGGL((k_tile<T, IP, SHORT_NUM, false>), dim3(tile_grid(n * p.G)), dim3(TILE_WPB * WAVE),
                            0, h->stream, r0, n, p.B.cols, p.tws, p.G, p.TR, Ap, Aj, Ax, Bp, Bj, Bx,
                            (const uint32_t*)p.tidx, p.bitmap, (int64_t*)nullptr, (const int64_t*)p.item_cnt, cj,
@@ -439,15 +477,21 @@ spg_status_t run_numeric_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_t
     } else if (p.use_short) {
         int32_t* cnt = spill_counts(p, true);
         int32_t* l1 = p.spill;
-        hipLaunchKernelGGL((k_short<T, IP, OFF, MODE, ShortSmall>), dim3((unsigned)grid_for(n, ShortSmall::WPB)),
-                           dim3(ShortSmall::WPB * WAVE), 0, h->stream, r0, n, p.B.cols, Ap, Aj, Ax, Bp, Bj,
-                           Bx, off, cj, cx, alpha, p.row_cnt, l1, cnt, (const int32_t*)nullptr,
-                           (const int32_t*)nullptr);
-        SPG_LAUNCHED(h);
+        {
+            PhaseTimer pt(h, SPG_PHASE_NUMERIC);
+            hipLaunchKernelGGL((k_short<T, IP, OFF, MODE, ShortSmall>), dim3((unsigned)grid_for(n, ShortSmall::WPB)),
+                               dim3(ShortSmall::WPB * WAVE), 0, h->stream, r0, n, p.B.cols, Ap, Aj, Ax, Bp, Bj,
+                               Bx, off, cj, cx, alpha, p.row_cnt, l1, cnt, (const int32_t*)nullptr,
+                               (const int32_t*)nullptr, (unsigned long long*)nullptr, (OFF*)nullptr,
+                               (int64_t*)nullptr);
+            SPG_LAUNCHED(h);
+        }
+        PhaseTimer ps(h, SPG_PHASE_SPILL);
         hipLaunchKernelGGL((k_numeric<T, IP, OFF, UB>), dim3(p.list_grid), dim3(BLOCK), 0, h->stream,
                            r0, n, p.B.cols, Ap, Aj, Ax, Bp, Bj, Bx, off, cj, cx, alpha, p.row_cnt,
                            p.seg, nz0, p.seg_len, (const int32_t*)l1, (const int32_t*)cnt);
     } else {
+        PhaseTimer pt(h, SPG_PHASE_NUMERIC);
         hipLaunchKernelGGL((k_numeric<T, IP, OFF, UB>), dim3((unsigned)grid_for(n, WPB)), dim3(BLOCK), 0,
                            h->stream, r0, n, p.B.cols, Ap, Aj, Ax, Bp, Bj, Bx, off, cj, cx, alpha,
                            p.row_cnt, p.seg, nz0, p.seg_len, (const int32_t*)nullptr,
@@ -479,6 +523,26 @@ spg_status_t run_scan(spg_handle_t h, spg_plan_s& p, void* out) {
                             p.scan_status + scan_tiles(p.A.rows) + 1, p.scalars, false);
 }
 
+// ALG1 single pass: structure + values + row pointer in one launch, compact into tj/tx
+template <typename T, typename IP, typename OUT>
+spg_status_t alg1_fused_run(spg_handle_t h, spg_plan_s& p, void* cp) {
+    PhaseTimer pt(h, SPG_PHASE_NUMERIC);
+    hipLaunchKernelGGL((k_short<T, IP, OUT, SHORT_NUMLB, ShortSmall>), dim3((unsigned)grid_for(p.A.rows, ShortSmall::WPB)),
+                       dim3(ShortSmall::WPB * WAVE), 0, h->stream, (int64_t)0, p.A.rows, p.B.cols,
+                       (const IP*)p.A.indptr, (const int32_t*)p.A.indices, (const T*)p.A.values,
+                       (const IP*)p.B.indptr, (const int32_t*)p.B.indices, (const T*)p.B.values,
+                       (const OUT*)nullptr, p.tj, (T*)p.tx, (T)1, p.row_cnt, (int32_t*)nullptr,
+                       (int32_t*)nullptr, (const int32_t*)nullptr, (const int32_t*)nullptr, p.lb, (OUT*)cp,
+                       p.scalars);
+    SPG_LAUNCHED(h);
+    return SPG_STATUS_SUCCESS;
+}
+
+template <typename T, typename IP>
+spg_status_t alg1_fused_typed(spg_handle_t h, spg_plan_s& p, void* cp, spg_index_t ct) {
+    return ct == SPG_INDEX_64I ? alg1_fused_run<T, IP, int64_t>(h, p, cp) : alg1_fused_run<T, IP, int32_t>(h, p, cp);
+}
+
 template <typename IP>
 spg_status_t symbolic_typed(spg_handle_t h, spg_plan_s& p) {
     spg_status_t st;
@@ -504,6 +568,22 @@ spg_status_t alg1_compute(spg_handle_t h, spg_plan_s& p) {
 template <typename T, typename IP, typename IPC>
 spg_status_t numeric_typed(spg_handle_t h, spg_plan_s& p, const spg_csr_t& C, T alpha) {
     const IPC* cp = (const IPC*)C.indptr;
+    if (p.alg1_fused) {
+        // C already computed compact in tj/tx: copy (unless C points there) and scale
+        const bool same = C.indices == (void*)p.tj && C.values == p.tx;
+        if (same && alpha != (T)1) {
+            if (p.scaled_in_place) return SPG_STATUS_INVALID_VALUE;   // would scale twice
+            p.scaled_in_place = true;
+        }
+        if (!same || alpha != (T)1) {
+            PhaseTimer pt(h, SPG_PHASE_COMPACT);
+            hipLaunchKernelGGL(k_copy_scale<T>, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(grid_for(p.nnzC, BLOCK), 65536))),
+                               dim3(BLOCK), 0, h->stream, p.nnzC, (const int32_t*)p.tj, (const T*)p.tx,
+                               (int32_t*)C.indices, (T*)C.values, alpha);
+            SPG_LAUNCHED(h);
+        }
+        return SPG_STATUS_SUCCESS;
+    }
     if (p.alg == SPG_ALG1 && !p.use_tile) {
         if (p.A.rows > 0) {
             PhaseTimer pt(h, SPG_PHASE_COMPACT);
@@ -654,11 +734,8 @@ spg_status_t spg_plan(spg_handle_t h, const spg_csr_t* A, const spg_csr_t* B, sp
     if (tmp.alg == SPG_ALG1 && !tmp.use_tile) {
         if (workspace && same_as_query) {
             tmp.P = h->q_P;
-        } else {
-            ScratchView sv;
-            if ((st = scratch_for_products(h, A->rows, sv))) return st;
-            if ((st = products_prefix(h, *A, *B, sv.cnt, sv.pref, sv.scal, sv.status))) return st;
-            if ((st = read_scalars(h, sv.scal, 1, &tmp.P))) return st;
+        } else if ((st = products_total(h, *A, *B, &tmp.P))) {
+            return st;
         }
     } else if (tmp.alg == SPG_ALG3) {
         if (workspace && same_as_query) {
@@ -698,7 +775,7 @@ spg_status_t spg_plan(spg_handle_t h, const spg_csr_t* A, const spg_csr_t* B, sp
         hipError_t e1 = hipMemsetAsync(p->ws, 0, L.row_cnt, h->stream);   // scalars + status
         if (e1 != hipSuccess) { delete p; return hip_fail(h, e1); }
     }
-    if (p->alg == SPG_ALG1 && !p->use_tile) {
+    if (p->alg == SPG_ALG1 && !p->use_tile && !fused_alg1(*p)) {
         // upper-bound offsets for the single pass: product prefix straight into the workspace
         spg_status_t st2 = products_prefix(h, p->A, p->B, p->row_cnt, p->ub, p->scalars + 2,
                                            p->scan_status, false);
@@ -714,10 +791,7 @@ spg_status_t spg_num_products(spg_handle_t h, spg_plan_t p, int64_t* num_product
     if (p->P < 0) {
         SPG_HIP(h, hipSetDevice(h->device));
         spg_status_t st;
-        ScratchView sv;
-        if ((st = scratch_for_products(h, p->A.rows, sv))) return st;
-        if ((st = products_prefix(h, p->A, p->B, sv.cnt, sv.pref, sv.scal, sv.status))) return st;
-        if ((st = read_scalars(h, sv.scal, 1, &p->P))) return st;
+        if ((st = products_total(h, p->A, p->B, &p->P))) return st;
     }
     *num_products = p->P;
     return SPG_STATUS_SUCCESS;
@@ -731,6 +805,52 @@ spg_status_t spg_symbolic(spg_handle_t h, spg_plan_t p, void* C_indptr, spg_inde
     SPG_HIP(h, hipSetDevice(h->device));
     spg_status_t st;
     const bool i64 = p->A.indptr_type == SPG_INDEX_64I;
+    const bool f64 = p->A.value_type == SPG_R_64F;
+    if (fused_alg1(*p) && !p->fused_failed) {
+        // ALG1 single pass: one launch writes C compact into tj/tx and its row pointer; a
+        // repeated call (int64 retry) only rescans the row counts it recorded
+        ++p->symbolic_runs;
+        if (!p->counts_ready) {
+            st = f64 ? (i64 ? alg1_fused_typed<double, int64_t>(h, *p, C_indptr, C_indptr_type)
+                            : alg1_fused_typed<double, int32_t>(h, *p, C_indptr, C_indptr_type))
+                     : (i64 ? alg1_fused_typed<float, int64_t>(h, *p, C_indptr, C_indptr_type)
+                            : alg1_fused_typed<float, int32_t>(h, *p, C_indptr, C_indptr_type));
+        } else {
+            const int64_t tiles = scan_tiles(p->A.rows) + 1;
+            SPG_HIP(h, hipMemsetAsync(p->scan_status + tiles, 0, sizeof(unsigned long long) * tiles, h->stream));
+            st = C_indptr_type == SPG_INDEX_64I ? run_scan<int64_t>(h, *p, C_indptr)
+                                                : run_scan<int32_t>(h, *p, C_indptr);
+            if (!st) {   // the scan leaves the total in scalars[0]
+                int64_t tot;
+                if ((st = read_scalars(h, p->scalars, 1, &tot))) return st;
+                if (C_indptr_type == SPG_INDEX_32I && tot > 2147483647LL) return SPG_STATUS_OVERFLOW;
+                p->nnzC = tot;
+                p->c_indptr = C_indptr;
+                p->c_indptr_type = C_indptr_type;
+                *nnzC = tot;
+                return SPG_STATUS_SUCCESS;
+            }
+        }
+        if (st) return st;
+        int64_t sc[10];
+        if ((st = read_scalars(h, p->scalars, 10, sc))) return st;
+        if (!sc[LB_FAIL]) {
+            p->counts_ready = true;
+            p->alg1_fused = true;
+            const int64_t tot = sc[LB_TOTAL];
+            if (C_indptr_type == SPG_INDEX_32I && tot > 2147483647LL) return SPG_STATUS_OVERFLOW;
+            p->nnzC = tot;
+            p->c_indptr = C_indptr;
+            p->c_indptr_type = C_indptr_type;
+            *nnzC = tot;
+            return SPG_STATUS_SUCCESS;
+        }
+        // a row the single pass cannot take: run the upper-bound path instead
+        p->fused_failed = true;
+        p->symbolic_runs = 0;
+        if ((st = products_prefix(h, p->A, p->B, p->row_cnt, p->ub, p->scalars + 2, p->scan_status, false)))
+            return st;
+    }
     if (p->symbolic_runs++ > 0 && !p->use_tile) {
         // a repeated call (e.g. retrying with int64 row pointers): the row counts are kept;
         // re-arm the row-pointer scan's status words
@@ -739,7 +859,7 @@ spg_status_t spg_symbolic(spg_handle_t h, spg_plan_t p, void* C_indptr, spg_inde
     }
     if (!p->counts_ready) {
         if (p->alg == SPG_ALG1 && !p->use_tile) {
-            if (p->A.value_type == SPG_R_64F)
+            if (f64)
                 st = i64 ? alg1_compute<double, int64_t>(h, *p) : alg1_compute<double, int32_t>(h, *p);
             else
                 st = i64 ? alg1_compute<float, int64_t>(h, *p) : alg1_compute<float, int32_t>(h, *p);
@@ -788,6 +908,13 @@ spg_status_t spg_numeric(spg_handle_t h, spg_plan_t p, const void* alpha, spg_cs
                         : numeric_typed<float, int64_t, int32_t>(h, *p, *C, a);
     return c64 ? numeric_typed<float, int32_t, int64_t>(h, *p, *C, a)
                : numeric_typed<float, int32_t, int32_t>(h, *p, *C, a);
+}
+
+spg_status_t spg_result_in_workspace(spg_plan_t p, void** indices, void** values) {
+    if (!p || !indices || !values) return SPG_STATUS_INVALID_VALUE;
+    *indices = p->alg1_fused ? (void*)p->tj : nullptr;
+    *values = p->alg1_fused ? p->tx : nullptr;
+    return SPG_STATUS_SUCCESS;
 }
 
 spg_status_t spg_peak_bytes(spg_plan_t p, size_t* bytes) {

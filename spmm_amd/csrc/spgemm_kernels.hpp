@@ -30,6 +30,28 @@ __global__ __launch_bounds__(BLOCK) void k_row_products(int64_t rows, const IP* 
     if (l == 0) out[row] = s;
 }
 
+// Total number of products P = sum over A's entries of the length of the B row they select
+// (flat over A's entries, one atomic per block; `out` must be zero).
+template <typename IP>
+__global__ __launch_bounds__(BLOCK) void k_products_total(int64_t nnzA, const int32_t* __restrict__ Aj,
+                                                          const IP* __restrict__ Bp,
+                                                          unsigned long long* __restrict__ out) {
+    __shared__ long long part[WPB];
+    long long s = 0;
+    for (int64_t e = (int64_t)blockIdx.x * BLOCK + threadIdx.x; e < nnzA; e += (int64_t)gridDim.x * BLOCK) {
+        const int32_t k = Aj[e];
+        s += (long long)(Bp[k + 1] - Bp[k]);
+    }
+    s = wave_sum64(s);
+    if (lane_id() == 0) part[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        long long t = 0;
+        for (int w = 0; w < WPB; ++w) t += part[w];
+        if (t) atomicAdd(out, (unsigned long long)t);
+    }
+}
+
 // ---------------------------------------------------------------------------------------
 // Symbolic phase (general path): structural nnz of each output row (no values).  One wave
 // per row, a private bitmap window in LDS.  Rows of C wider than one window walk B with
@@ -288,7 +310,58 @@ __global__ __launch_bounds__(BLOCK) void k_numeric(
 // the limits are appended to `spill` (handled by the next kernel; the list order does not
 // affect any result).  Rows come from [row0, row0 + nrows) or, with `list`, from
 // list[0 .. *list_count).
-enum { SHORT_SYM = 0, SHORT_NUM = 1, SHORT_NUMUB = 2 };
+// SHORT_NUMLB (ALG1 single pass): one wave per row in row order; each row publishes its entry
+// count, looks back over its predecessors for its exclusive offset (decoupled look-back, as
+// k_scan_lb) and writes its columns and values straight to their final place and its row
+// pointer to Cp.  A row the kernel cannot take sets scal[LB_FAIL] (the host then runs the
+// SHORT_NUMUB path); it still publishes, so no successor waits forever.
+enum { SHORT_SYM = 0, SHORT_NUM = 1, SHORT_NUMUB = 2, SHORT_NUMLB = 3 };
+enum { LB_TICKET = 6, LB_FAIL = 7, LB_TOTAL = 8, LB_OVERFLOW = 9 };
+
+// Block `row` publishes its aggregate (flag 1) or, for block 0, its inclusive prefix (flag 2).
+__device__ __forceinline__ void lb_publish(unsigned long long* st, int64_t row, int64_t v, int l) {
+    if (l == 0)
+        __hip_atomic_store(&st[row], ((row == 0 ? 2ull : 1ull) << 62) | (unsigned long long)v,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Exclusive prefix of `row` by looking back over its predecessors 64 at a time; publishes
+// the row's inclusive prefix.  Rows are mapped statically (row = wave id), so a wave may
+// wait on a row whose wave has not been dispatched yet: the wait is bounded by LB_SPIN
+// wall-clock ticks (100 MHz), after which the row sets `*fail` (the host then discards the
+// pass) and carries on, so the grid always drains.
+constexpr uint64_t LB_SPIN = 2000000;   // 20 ms
+__device__ __forceinline__ int64_t lb_lookback(unsigned long long* st, int64_t row, int64_t v, int l,
+                                               int64_t* fail) {
+    constexpr unsigned long long VMASK = (1ull << 62) - 1;
+    if (row == 0) return 0;
+    long long prefix = 0;
+    int64_t j = row - 1;
+    const uint64_t t0 = wall_clock64();
+    for (;;) {
+        const int64_t q = j - l;
+        unsigned long long s = 0;
+        if (q >= 0) {
+            do {
+                s = __hip_atomic_load(&st[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((s >> 62) == 0 && wall_clock64() - t0 > LB_SPIN) {
+                    *fail = 1;
+                    s = 2ull << 62;   // give up: treat as an inclusive zero
+                }
+            } while ((s >> 62) == 0);
+        }
+        const unsigned long long incm = __ballot(q >= 0 && (s >> 62) == 2);
+        const int stop = incm ? __ffsll((long long)incm) - 1 : WAVE;
+        const long long val = (q >= 0 && l <= stop) ? (long long)(s & VMASK) : 0;
+        prefix += wave_sum64(val);
+        if (incm || j - WAVE < 0) break;
+        j -= WAVE;
+    }
+    if (l == 0)
+        __hip_atomic_store(&st[row], (2ull << 62) | (unsigned long long)(prefix + v), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    return prefix;
+}
 
 template <int CAP_, int PLONG_, int WPB_, int R_> struct ShortCfg {
     static constexpr int R = R_;               // register-resident products per lane
@@ -336,25 +409,93 @@ __global__ __launch_bounds__(G::WPB * WAVE) void k_short(
     const int32_t* __restrict__ Bj, const T* __restrict__ Bx, const OFF* __restrict__ Coff,
     int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha, int64_t* __restrict__ row_cnt,
     int32_t* __restrict__ spill, int32_t* __restrict__ spill_count,
-    const int32_t* __restrict__ list, const int32_t* __restrict__ list_count) {
+    const int32_t* __restrict__ list, const int32_t* __restrict__ list_count,
+    unsigned long long* __restrict__ lb, OFF* __restrict__ Cp, int64_t* __restrict__ scal) {
     constexpr int R = G::R;
+    constexpr bool LB = MODE == SHORT_NUMLB;
     constexpr bool VALS = MODE != SHORT_SYM;
     __shared__ __attribute__((aligned(16))) ShortLds<T, IP, G, VALS> lds[G::WPB];
     const int l = lane_id();
     const int wv = uniform((int)(threadIdx.x >> 6));
     ShortLds<T, IP, G, VALS>& S = lds[wv];
     const int64_t count = list ? (int64_t)*list_count : nrows;
-    for (int64_t it = (int64_t)blockIdx.x * G::WPB + wv; it < count; it += (int64_t)gridDim.x * G::WPB) {
+    // LB: a row with no entries (or one this kernel cannot take) still publishes and writes
+    // its row pointer
+    // LB: one look-back per block (its WPB consecutive rows, one per wave).  A wave drops
+    // its row count in LDS and goes on; wave 0 waits for the WPB counts, publishes the
+    // block's aggregate, looks back over earlier blocks and posts the block's base; a wave
+    // waits for the base only when it is about to write.  Every wave arrives exactly once
+    // (rows past the end with 0).
+    __shared__ long long lb_v[G::WPB];
+    __shared__ long long lb_base;
+    __shared__ int lb_arrived, lb_ready;
+    if (LB) {
+        if (threadIdx.x == 0) {
+            lb_arrived = 0;
+            lb_ready = 0;
+        }
+        __syncthreads();
+    }
+    auto lb_arrive = [&](int64_t v) {
+        if (l == 0) {
+            lb_v[wv] = v;
+            __hip_atomic_fetch_add(&lb_arrived, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    };
+    auto lb_lead = [&]() {   // wave 0
+        while (__hip_atomic_load(&lb_arrived, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < G::WPB)
+            __builtin_amdgcn_s_sleep(1);
+        long long agg = 0;
+#pragma unroll
+        for (int w = 0; w < G::WPB; ++w) agg += lb_v[w];
+        lb_publish(lb, blockIdx.x, agg, l);
+        const int64_t pre = lb_lookback(lb, blockIdx.x, agg, l, &scal[LB_FAIL]);
+        if (l == 0) {
+            lb_base = pre;
+            __hip_atomic_store(&lb_ready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    };
+    auto lb_row_base = [&](int64_t row, int64_t v) -> int64_t {
+        while (__hip_atomic_load(&lb_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+            __builtin_amdgcn_s_sleep(1);
+        long long pre = lb_base;
+        for (int w = 0; w < wv; ++w) pre += lb_v[w];
+        if (l == 0) {
+            Cp[row] = (OFF)pre;
+            if (row == nrows - 1) {
+                const int64_t tot = pre + v;
+                Cp[nrows] = (OFF)tot;
+                scal[LB_TOTAL] = tot;
+                scal[LB_OVERFLOW] = (sizeof(OFF) == 4 && tot > 2147483647LL) ? 1 : 0;
+            }
+        }
+        return pre;
+    };
+    auto lb_block = [&](int64_t row, int64_t v) -> int64_t {
+        lb_arrive(v);
+        if (wv == 0) lb_lead();
+        return lb_row_base(row, v);
+    };
+    auto lb_empty = [&](int64_t row, bool fail) {
+        if (l == 0) {
+            if (fail) scal[LB_FAIL] = 1;
+            row_cnt[row] = 0;
+        }
+        lb_block(row, 0);
+    };
+    auto process = [&](int64_t it) {
         const int64_t row = list ? (int64_t)uniform(list[it]) : row0 + it;
         const int64_t a0 = Ap[row];
         const int nA = (int)(Ap[row + 1] - a0);
         if (nA <= 0 || ncols <= 0) {
-            if (MODE != SHORT_NUM && l == 0) row_cnt[row] = 0;
-            continue;
+            if (LB) lb_empty(row, false);
+            else if (MODE != SHORT_NUM && l == 0) row_cnt[row] = 0;
+            return;
         }
         if (nA > WAVE || ncols > 32LL * G::NW) {
-            if (l == 0) spill[atomicAdd(spill_count, 1)] = (int32_t)row;
-            continue;
+            if (LB) lb_empty(row, true);
+            else if (l == 0) spill[atomicAdd(spill_count, 1)] = (int32_t)row;
+            return;
         }
         int cnt = 0;
         IP b0 = 0;
@@ -369,12 +510,14 @@ __global__ __launch_bounds__(G::WPB * WAVE) void k_short(
         const int off = incl - cnt;
         const int P = readlane_i(incl, WAVE - 1);
         if (P > G::PLONG) {
-            if (l == 0) spill[atomicAdd(spill_count, 1)] = (int32_t)row;
-            continue;
+            if (LB) lb_empty(row, true);
+            else if (l == 0) spill[atomicAdd(spill_count, 1)] = (int32_t)row;
+            return;
         }
         if (P == 0) {
-            if (MODE != SHORT_NUM && l == 0) row_cnt[row] = 0;
-            continue;
+            if (LB) lb_empty(row, false);
+            else if (MODE != SHORT_NUM && l == 0) row_cnt[row] = 0;
+            return;
         }
         S.jb0[l] = b0;
         S.joff[l] = (uint16_t)off;
@@ -440,7 +583,14 @@ __global__ __launch_bounds__(G::WPB * WAVE) void k_short(
         const int nnz = readlane_i(pincl, WAVE - 1);
         if (MODE == SHORT_SYM) {
             if (l == 0) row_cnt[row] = nnz;
-            continue;
+            return;
+        }
+        // LB: publish, then look back at once -- an inclusive prefix published promptly is
+        // what keeps successors' look-backs short
+        int64_t cbase = -1;
+        if (LB) {
+            lb_arrive(nnz);
+            if (wv == 0) lb_lead();
         }
         const int p0 = pincl - mine;
         {
@@ -548,8 +698,10 @@ __global__ __launch_bounds__(G::WPB * WAVE) void k_short(
                 }
             }
             wsync();
-            int32_t* __restrict__ crow = Cj + (int64_t)Coff[row] + wb;
-            T* __restrict__ xrow = Cx + (int64_t)Coff[row] + wb;
+            if (LB && cbase < 0) cbase = lb_row_base(row, nnz);
+            const int64_t rbase = LB ? cbase : (int64_t)Coff[row];
+            int32_t* __restrict__ crow = Cj + rbase + wb;
+            T* __restrict__ xrow = Cx + rbase + wb;
             for (int p = l; p < wn; p += WAVE) {
                 crow[p] = (int32_t)S.tag[p];
                 const T val = S.acc[p];
@@ -558,9 +710,13 @@ __global__ __launch_bounds__(G::WPB * WAVE) void k_short(
             wsync();
             L0 = L1;
         }
-        if (MODE == SHORT_NUMUB && l == 0) row_cnt[row] = nnz;
+        if ((MODE == SHORT_NUMUB || LB) && l == 0) row_cnt[row] = nnz;
         wsync();
-    }
+    };
+    // (LB: the grid has one wave per row, so every wave meets lb_block exactly once)
+    for (int64_t it = (int64_t)blockIdx.x * G::WPB + wv; it < count; it += (int64_t)gridDim.x * G::WPB)
+        process(it);
+    if (LB && (int64_t)blockIdx.x * G::WPB + wv >= count) lb_arrive(0);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -650,6 +806,21 @@ __global__ __launch_bounds__(BLOCK) void k_scan_lb(int64_t n, const int64_t* __r
         out[n] = (OUT)total;
         scalars[0] = total;
         scalars[1] = (sizeof(OUT) == 4 && total > 2147483647LL) ? 1 : 0;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// ALG1 single pass, numeric call: C from the compact arrays in the workspace, scaled by
+// alpha (in place when C points into the workspace).
+template <typename T>
+__global__ __launch_bounds__(BLOCK) void k_copy_scale(int64_t n, const int32_t* __restrict__ sj,
+                                                      const T* __restrict__ sx, int32_t* __restrict__ dj,
+                                                      T* __restrict__ dx, T alpha) {
+    const bool copy_j = dj != sj;
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLOCK) {
+        if (copy_j) dj[i] = sj[i];
+        const T v = sx[i];
+        dx[i] = alpha == (T)1 ? v : mul_rn(alpha, v);
     }
 }
 

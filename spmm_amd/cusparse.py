@@ -161,8 +161,20 @@ def spgemm(a, b, alpha=1, alg=0, chunk_fraction=0.2, verbose=False):
                                   _lib.SPG_INDEX_64I, ctypes.byref(nnz))
         check(st, "spg_symbolic")
         nnzc = int(nnz.value)
-        indices = torch.empty(nnzc, dtype=torch.int32, device=dev)
-        data = torch.empty(nnzc, dtype=a.data.dtype, device=dev)
+        # ALG1 single pass: C already sits compact in the workspace -- take views of it
+        pj, px = ctypes.c_void_p(), ctypes.c_void_p()
+        check(lib.spg_result_in_workspace(plan, ctypes.byref(pj), ctypes.byref(px)),
+              "spg_result_in_workspace")
+        in_ws = bool(pj.value) and nnzc > 0
+        if in_ws:
+            base = ws.data_ptr()
+            vsz = a.data.element_size()
+            oj, ox = pj.value - base, px.value - base
+            indices = ws[oj:oj + 4 * nnzc].view(torch.int32)
+            data = ws[ox:ox + vsz * nnzc].view(a.data.dtype)
+        else:
+            indices = torch.empty(nnzc, dtype=torch.int32, device=dev)
+            data = torch.empty(nnzc, dtype=a.data.dtype, device=dev)
         c = csr_matrix._from_parts(data, indices, indptr, (m, n), canonical=True)
         vc = SpgCsr(m, n, nnzc, indptr.data_ptr(), indices.data_ptr() if nnzc else 0,
                     data.data_ptr() if nnzc else 0, _IT[indptr.dtype], _VT[data.dtype])
@@ -171,6 +183,8 @@ def spgemm(a, b, alpha=1, alg=0, chunk_fraction=0.2, verbose=False):
         check(lib.spg_numeric(h.ptr, plan, ctypes.byref(al), ctypes.byref(vc)), "spg_numeric")
         peak = ctypes.c_size_t(0)
         lib.spg_peak_bytes(plan, ctypes.byref(peak))
+        if in_ws:   # C's arrays are views of the workspace: workspace + row pointer
+            peak = ctypes.c_size_t(int(ws_bytes.value) + indptr.element_size() * (m + 1))
         last_stats.alg, last_stats.workspace_bytes = int(algo), int(ws_bytes.value)
         last_stats.peak_bytes, last_stats.nnz = int(peak.value), nnzc
         # keep the workspace alive until the queued kernels have consumed it

@@ -302,3 +302,77 @@ def test_tile_path_dense_tiles_fp32_int64():
         C = cusparse.spgemm(dA, dB, alg=alg, chunk_fraction=0.1)
         _assert_same((C.indptr.cpu().numpy().astype(np.int64), C.indices.cpu().numpy(),
                       C.data.cpu().numpy()), ref)
+
+
+def test_alg1_single_pass_fallback_long_row():
+    """ALG1 runs as one fused pass for short-row shapes; a row with more than 64 entries
+    makes the pass hand over to the upper-bound path, with the same result."""
+    rng = np.random.default_rng(41)
+    A = sp.random(3000, 2000, density=0.004, format="lil", random_state=rng)
+    A[1234, :300] = rng.standard_normal(300)
+    A = sp.csr_matrix(A)
+    B = sp.random(2000, 3000, density=0.004, format="csr", random_state=rng)
+    A.sort_indices(); B.sort_indices()
+    ref = oracle.spgemm(A, B, alpha=2.5, keep_zeros=True, sort=True)
+    _assert_same(_gpu(A, B, alg=1, alpha=2.5), ref)
+    _assert_same(_gpu(A, B, alg=2, alpha=2.5), ref)
+
+
+def test_alg1_single_pass_abi_sequence():
+    """C-ABI sequence of the fused ALG1: repeated spg_symbolic (int32 then int64 row
+    pointer, the overflow retry) rewrites the row pointer from the look-back words; C in
+    the workspace is scaled once in place; C elsewhere gets a copy; a second in-place
+    scaling is refused."""
+    import ctypes
+    from spmm_amd import _lib, gen
+    from spmm_amd._lib import SpgCsr
+    from spmm_amd.sparse import csr_matrix
+    Ah, Bh = gen.scipy_pair(4096, 2e-3, seed=77)
+    ref = oracle.spgemm(Ah, Bh, alpha=-3.0, keep_zeros=True, sort=True)
+    A, B = csr_matrix(Ah, device=_dev()), csr_matrix(Bh, device=_dev())
+    h = _lib.get_handle(0)
+    h.set_stream(torch.cuda.current_stream().cuda_stream)
+    lib = h.lib
+
+    def view(M):
+        return SpgCsr(M.shape[0], M.shape[1], M.nnz, M.indptr.data_ptr(), M.indices.data_ptr(),
+                      M.data.data_ptr(), _lib.SPG_INDEX_32I, _lib.SPG_R_64F)
+
+    va, vb = view(A), view(B)
+    for in_place in (True, False):
+        wsb = ctypes.c_size_t(0)
+        _lib.check(lib.spg_plan(h.ptr, ctypes.byref(va), ctypes.byref(vb), _lib.SPG_ALG1, 0.2,
+                                ctypes.byref(wsb), None, None))
+        ws = torch.empty(wsb.value, dtype=torch.uint8, device=_dev())
+        plan = ctypes.c_void_p()
+        _lib.check(lib.spg_plan(h.ptr, ctypes.byref(va), ctypes.byref(vb), _lib.SPG_ALG1, 0.2,
+                                ctypes.byref(wsb), ctypes.c_void_p(ws.data_ptr()), ctypes.byref(plan)))
+        p32 = torch.empty(4097, dtype=torch.int32, device=_dev())
+        p64 = torch.empty(4097, dtype=torch.int64, device=_dev())
+        nnz = ctypes.c_int64(0)
+        _lib.check(lib.spg_symbolic(h.ptr, plan, ctypes.c_void_p(p32.data_ptr()), _lib.SPG_INDEX_32I,
+                                    ctypes.byref(nnz)))
+        _lib.check(lib.spg_symbolic(h.ptr, plan, ctypes.c_void_p(p64.data_ptr()), _lib.SPG_INDEX_64I,
+                                    ctypes.byref(nnz)))
+        assert nnz.value == len(ref[1])
+        assert np.array_equal(p32.cpu().numpy().astype(np.int64), ref[0])
+        assert np.array_equal(p64.cpu().numpy(), ref[0])
+        pj, px = ctypes.c_void_p(), ctypes.c_void_p()
+        _lib.check(lib.spg_result_in_workspace(plan, ctypes.byref(pj), ctypes.byref(px)))
+        assert pj.value and px.value
+        n = nnz.value
+        if in_place:
+            cj = ws[pj.value - ws.data_ptr():][:4 * n].view(torch.int32)
+            cx = ws[px.value - ws.data_ptr():][:8 * n].view(torch.float64)
+        else:
+            cj = torch.empty(n, dtype=torch.int32, device=_dev())
+            cx = torch.empty(n, dtype=torch.float64, device=_dev())
+        vc = SpgCsr(4096, 4096, n, p64.data_ptr(), cj.data_ptr(), cx.data_ptr(), _lib.SPG_INDEX_64I,
+                    _lib.SPG_R_64F)
+        al = ctypes.c_double(-3.0)
+        _lib.check(lib.spg_numeric(h.ptr, plan, ctypes.byref(al), ctypes.byref(vc)))
+        if in_place:
+            assert lib.spg_numeric(h.ptr, plan, ctypes.byref(al), ctypes.byref(vc)) == 3
+        torch.cuda.synchronize()
+        _assert_same((p64.cpu().numpy(), cj.cpu().numpy(), cx.cpu().numpy()), ref)
+        lib.spg_plan_destroy(plan)
