@@ -131,6 +131,24 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     gflops = 2.0 * P_all * args.steps / elapsed / 1e9
 
+    # ---- the other algorithms on the same inputs (after the timed region; reported beside)
+    other = {}
+    if world == 1:
+        for alg in (1, 2, 3):
+            if alg == args.alg:
+                continue
+            for _ in range(3):
+                cusparse.spgemm(A, B, alg=alg, chunk_fraction=args.chunk_fraction)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            reps_o = max(5, args.steps // 2)
+            for _ in range(reps_o):
+                cusparse.spgemm(A, B, alg=alg, chunk_fraction=args.chunk_fraction)
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / reps_o
+            other[f"alg{alg}"] = {"gflops": round(2.0 * P / dt / 1e9, 3), "ms_per_step": round(dt * 1e3, 5),
+                                  "peak_hbm_bytes": int(cusparse.last_stats.peak_bytes)}
+
     # ---- per-kernel device times (separate, instrumented pass after the timed region)
     h = _lib.get_handle(local)
     h.set_stream(torch.cuda.current_stream(dev).cuda_stream)
@@ -214,6 +232,7 @@ def main():
             "dominant_phase": dom_name,
             "b_broadcast_ms": None if bcast_ms is None else round(bcast_ms, 3),
             "cpu_baseline": cpu,
+            "other_algs": other or None,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

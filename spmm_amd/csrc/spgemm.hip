@@ -72,6 +72,7 @@ struct spg_plan_s {
     bool alg1_fused = false;        // C's arrays were written compact into tj/tx by one pass
     bool fused_failed = false;      // the single pass met a row it cannot take
     bool scaled_in_place = false;   // spg_numeric scaled the workspace result by alpha
+    int64_t sym_spills = -1;        // rows the symbolic short-row pass spilled (-1 unknown)
     uint32_t* tidx = nullptr;       // B column-tile index, B.rows * (G + 1)
     uint32_t* bitmap = nullptr;     // per-item column bitmaps (symbolic -> numeric)
     int64_t* item_cnt = nullptr;    // per-item counts, scanned in place into offsets
@@ -254,7 +255,7 @@ spg_status_t products_total(spg_handle_t h, const spg_csr_t& A, const spg_csr_t&
     SPG_HIP(h, hipMemsetAsync(acc, 0, sizeof(unsigned long long), h->stream));
     if (A.nnz > 0) {
         PhaseTimer pt(h, SPG_PHASE_PRODUCTS);
-        const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(grid_for(A.nnz, BLOCK), 64));
+        const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(grid_for(A.nnz, 4 * BLOCK), 256));
         if (A.indptr_type == SPG_INDEX_64I)
             hipLaunchKernelGGL(k_products_total<int64_t>, dim3(grid), dim3(BLOCK), 0, h->stream, A.nnz,
                                (const int32_t*)A.indices, (const int64_t*)B.indptr, acc);
@@ -486,6 +487,7 @@ spg_status_t run_numeric_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_t
                                (int64_t*)nullptr);
             SPG_LAUNCHED(h);
         }
+        if (p.sym_spills == 0) return SPG_STATUS_SUCCESS;
         PhaseTimer ps(h, SPG_PHASE_SPILL);
         hipLaunchKernelGGL((k_numeric<T, IP, OFF, UB>), dim3(p.list_grid), dim3(BLOCK), 0, h->stream,
                            r0, n, p.B.cols, Ap, Aj, Ax, Bp, Bj, Bx, off, cj, cx, alpha, p.row_cnt,
@@ -871,8 +873,11 @@ spg_status_t spg_symbolic(spg_handle_t h, spg_plan_t p, void* C_indptr, spg_inde
     st = C_indptr_type == SPG_INDEX_64I ? run_scan<int64_t>(h, *p, C_indptr)
                                         : run_scan<int32_t>(h, *p, C_indptr);
     if (st) return st;
-    int64_t sc[2];
-    if ((st = read_scalars(h, p->scalars, 2, sc))) return st;
+    int64_t sc[5];
+    if ((st = read_scalars(h, p->scalars, 5, sc))) return st;
+    // the short-row kernel spills the same rows in both passes: none in the symbolic pass
+    // (one launch over all rows) means the numeric spill launch can be skipped
+    if (p->use_short && p->alg == SPG_ALG2) p->sym_spills = (int64_t)(uint32_t)(sc[4] & 0xffffffffu);
     p->counts_ready = true;      // counts (and tile offsets) stay valid for a repeated call
     if (sc[1] || (p->use_tile && C_indptr_type == SPG_INDEX_32I && sc[0] > 2147483647LL))
         return SPG_STATUS_OVERFLOW;

@@ -38,7 +38,16 @@ __global__ __launch_bounds__(BLOCK) void k_products_total(int64_t nnzA, const in
                                                           unsigned long long* __restrict__ out) {
     __shared__ long long part[WPB];
     long long s = 0;
-    for (int64_t e = (int64_t)blockIdx.x * BLOCK + threadIdx.x; e < nnzA; e += (int64_t)gridDim.x * BLOCK) {
+    const int64_t stride = (int64_t)gridDim.x * BLOCK;
+    int64_t e = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    for (; e + 3 * stride < nnzA; e += 4 * stride) {   // four independent gathers in flight
+        int32_t k[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) k[u] = Aj[e + u * stride];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) s += (long long)(Bp[k[u] + 1] - Bp[k[u]]);
+    }
+    for (; e < nnzA; e += stride) {
         const int32_t k = Aj[e];
         s += (long long)(Bp[k + 1] - Bp[k]);
     }
