@@ -73,7 +73,9 @@ struct spg_plan_s {
     bool fused_failed = false;      // the single pass met a row it cannot take
     bool scaled_in_place = false;   // spg_numeric scaled the workspace result by alpha
     int64_t sym_spills = -1;        // rows the symbolic short-row pass spilled (-1 unknown)
-    uint32_t* tidx = nullptr;       // B column-tile index, B.rows * (G + 1)
+    uint2* tidx = nullptr;          // B column-tile index, B.rows * G (start, end) pairs
+    void* brec = nullptr;           // B packed as (column, value) records (numeric tile pass)
+    bool brec_built = false;
     uint32_t* bitmap = nullptr;     // per-item column bitmaps (symbolic -> numeric)
     int64_t* item_cnt = nullptr;    // per-item counts, scanned in place into offsets
     bool tidx_built = false;
@@ -295,7 +297,7 @@ spg_status_t read_scalars(spg_handle_t h, const int64_t* dev, int n, int64_t* ou
 
 struct Layout {
     size_t scalars = 0, row_cnt = 0, seg = 0, spill = 0, status = 0, ub = 0, tj = 0, tx = 0;
-    size_t tidx = 0, items = 0, bitmap = 0, total = 0;
+    size_t tidx = 0, items = 0, bitmap = 0, brec = 0, total = 0;
 };
 
 inline int64_t tile_items(const spg_plan_s& p) { return p.use_tile ? p.A.rows * p.G : 0; }
@@ -321,7 +323,8 @@ Layout make_layout(const spg_plan_s& p) {
     L.seg = off;     off = align_up(off + sizeof(uint32_t) * 2 * (size_t)std::max<int64_t>(p.seg_len, 1));
     L.spill = off;   off = align_up(off + sizeof(int32_t) * 2 * (size_t)std::max<int64_t>(p.A.rows, 1));
     if (p.use_tile) {
-        L.tidx = off;  off = align_up(off + sizeof(uint32_t) * (size_t)p.B.rows * (size_t)(p.G + 1));
+        L.tidx = off;  off = align_up(off + sizeof(uint2) * (size_t)p.B.rows * (size_t)p.G);
+        L.brec = off;  off = align_up(off + (p.A.value_type == SPG_R_64F ? 16 : 8) * (size_t)std::max<int64_t>(p.B.nnz, 1));
         L.items = off; off = align_up(off + sizeof(int64_t) * (size_t)(tile_items(p) + 1));
         L.bitmap = off; off = align_up(off + sizeof(uint32_t) * (size_t)tile_items(p) * (size_t)((1 << p.tws) >> 5));
     }
@@ -342,7 +345,8 @@ void carve(spg_plan_s& p, const Layout& L) {
     p.scan_status = (unsigned long long*)(p.ws + L.status);
     if (fused_alg1(p)) p.lb = p.scan_status + 2 * (scan_tiles(p.A.rows) + 1);
     if (p.use_tile) {
-        p.tidx = (uint32_t*)(p.ws + L.tidx);
+        p.tidx = (uint2*)(p.ws + L.tidx);
+        p.brec = (void*)(p.ws + L.brec);
         p.item_cnt = (int64_t*)(p.ws + L.items);
         p.bitmap = (uint32_t*)(p.ws + L.bitmap);
     }
@@ -427,7 +431,7 @@ spg_status_t run_symbolic_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_
         PhaseTimer pt(h, SPG_PHASE_SYMBOLIC);
         const int R = 1 << (p.twss - p.tws);
         hipLaunchKernelGGL(k_tile_sym<IP>, dim3(tile_grid(n * ((p.G + R - 1) / R))), dim3(TILE_WPB * WAVE), 0,
-                           h->stream, r0, n, p.tws, p.G, p.twss, Ap, Aj, Bp, Bj, (const uint32_t*)p.tidx,
+                           h->stream, r0, n, p.tws, p.G, p.twss, Ap, Aj, Bp, Bj, (const uint2*)p.tidx,
                            p.bitmap, p.item_cnt);
     } else if (p.use_short) {
         int32_t* cnt = spill_counts(p, false);
@@ -470,11 +474,17 @@ spg_status_t run_numeric_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_t
     const T* Bx = (const T*)p.B.values;
     constexpr int MODE = UB ? SHORT_NUMUB : SHORT_NUM;
     if (p.use_tile) {
+        if (!p.brec_built) {
+            PhaseTimer ps(h, SPG_PHASE_SPILL);
+            hipLaunchKernelGGL(k_pack_b<T>, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(grid_for(p.B.nnz, 256), 8192))),
+                               dim3(256), 0, h->stream, p.B.nnz, Bj, Bx, (BRec<T>*)p.brec);
+            SPG_LAUNCHED(h);
+            p.brec_built = true;
+        }
         PhaseTimer pt(h, SPG_PHASE_NUMERIC);
-        hipLaunchKernelGGL((k_tile<T, IP, SHORT_NUM, false>), dim3(tile_grid(n * p.G)), dim3(TILE_WPB * WAVE),
-                           0, h->stream, r0, n, p.B.cols, p.tws, p.G, p.TR, Ap, Aj, Ax, Bp, Bj, Bx,
-                           (const uint32_t*)p.tidx, p.bitmap, (int64_t*)nullptr, (const int64_t*)p.item_cnt, cj,
-                           cx, alpha);
+        hipLaunchKernelGGL((k_tile<T, IP>), dim3(tile_grid(n * p.G)), dim3(TILE_WPB * WAVE), 0, h->stream, r0,
+                           n, p.tws, p.G, Ap, Aj, Ax, Bp, (const BRec<T>*)p.brec, (const uint2*)p.tidx,
+                           (const uint32_t*)p.bitmap, (const int64_t*)p.item_cnt, cj, cx, alpha);
     } else if (p.use_short) {
         int32_t* cnt = spill_counts(p, true);
         int32_t* l1 = p.spill;

@@ -381,7 +381,7 @@ template <int CAP_, int PLONG_, int WPB_, int R_> struct ShortCfg {
     static constexpr int WPB = WPB_;           // waves per block
     static constexpr int MKB = (PREG + 511) / 512 * 512;   // marker bytes (8 per lane per piece)
 };
-using ShortSmall = ShortCfg<512, 65535, 4, 8>;     // ~10 KB LDS per wave: 16 waves / CU;
+using ShortSmall = ShortCfg<320, 65535, 4, 8>;     // ~10 KB LDS per wave: 16 waves / CU;
                                                    // 640 products per row in registers
 
 template <typename T, typename IP, typename G, bool VALS> struct ShortLds {
@@ -412,7 +412,7 @@ __device__ __forceinline__ int chunk_src(L& S, int l, int cnt, int off, int c0, 
 }
 
 template <typename T, typename IP, typename OFF, int MODE, typename G>
-__global__ __launch_bounds__(G::WPB * WAVE) void k_short(
+__global__ __launch_bounds__(G::WPB * WAVE, 5) void k_short(
     int64_t row0, int64_t nrows, int64_t ncols, const IP* __restrict__ Ap,
     const int32_t* __restrict__ Aj, const T* __restrict__ Ax, const IP* __restrict__ Bp,
     const int32_t* __restrict__ Bj, const T* __restrict__ Bx, const OFF* __restrict__ Coff,

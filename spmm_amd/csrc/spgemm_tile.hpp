@@ -32,30 +32,52 @@ template <typename T, typename IP, bool VALS> struct TileLds {
 };
 
 // ---------------------------------------------------------------------------------------
-// B column-tile index: tidx[k*(G+1) + g] = offset inside B row k of its first entry with
-// column >= g*TW (g = 0..G; g = G gives the row length).  One wave per B row; entries
-// are sorted, so each tile boundary is written by the entry where the tile id steps.
+// B column-tile index: tidx[k*G + g] = (start, end) of B row k's entries with columns in
+// tile g, as offsets inside the row (one 8-byte load per segment).  start_g = first entry
+// with column >= g*TW.  One wave per B row; entries are sorted, so each boundary is
+// written by the entry where the tile id steps.
 template <typename IP>
 __global__ __launch_bounds__(256) void k_tile_index(int64_t rows, const IP* __restrict__ Bp,
                                                     const int32_t* __restrict__ Bj, int tws, int G,
-                                                    uint32_t* __restrict__ tidx) {
+                                                    uint2* __restrict__ tidx) {
     const int l = lane_id();
     const int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (k >= rows) return;
     const IP r0 = Bp[k];
     const int len = (int)(Bp[k + 1] - r0);
-    uint32_t* out = tidx + k * (int64_t)(G + 1);
+    uint32_t* out = reinterpret_cast<uint32_t*>(tidx + k * (int64_t)G);
+    auto put = [&](int g, uint32_t v) {   // boundary g: start of tile g, end of tile g-1
+        if (g < G) out[2 * g] = v;
+        if (g > 0) out[2 * g - 1] = v;
+    };
     for (int e0 = 0; e0 < len; e0 += WAVE) {
         const int e = e0 + l;
         const int t = e < len ? Bj[r0 + e] >> tws : G;          // tile of this entry
         int tp = __shfl_up(t, 1, WAVE);                         // tile of the previous entry
         if (l == 0) tp = e0 == 0 ? -1 : (Bj[r0 + e0 - 1] >> tws);
         if (e < len)
-            for (int g = tp + 1; g <= t; ++g) out[g] = (uint32_t)e;
+            for (int g = tp + 1; g <= t; ++g) put(g, (uint32_t)e);
     }
-    // tiles after the last entry (and all tiles of an empty row) start at len
+    // boundaries after the last entry (and all of an empty row) are at len
     const int tl = len > 0 ? Bj[r0 + len - 1] >> tws : -1;
-    for (int g = tl + 1 + l; g <= G; g += WAVE) out[g] = (uint32_t)len;
+    for (int g = tl + 1 + l; g <= G; g += WAVE) put(g, (uint32_t)len);
+}
+
+// B packed as (column, value) records for the numeric tile pass: one load brings both.
+template <typename T> struct BRec;
+template <> struct __attribute__((aligned(16))) BRec<double> { int32_t c; int32_t pad; double v; };
+template <> struct __attribute__((aligned(8))) BRec<float> { int32_t c; float v; };
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_pack_b(int64_t nnz, const int32_t* __restrict__ Bj,
+                                                const T* __restrict__ Bx, BRec<T>* __restrict__ rec) {
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < nnz; e += (int64_t)gridDim.x * 256) {
+        BRec<T> r;
+        r.c = Bj[e];
+        if constexpr (sizeof(BRec<T>) == 16) r.pad = 0;
+        r.v = Bx[e];
+        rec[e] = r;
+    }
 }
 
 // Blocks are dispatched round-robin over the 8 XCDs.  Logical block ids that keep
@@ -91,7 +113,8 @@ __device__ __forceinline__ void group_markers(L& S, int l, int cnt, int off, int
 template <int U, bool VALS, typename T, typename IP, typename L, typename F>
 __device__ __forceinline__ void walk_group(L& S, int l, int gb, int Pb, int& carry,
                                            const int32_t* __restrict__ Bj,
-                                           const T* __restrict__ Bx, F&& fn) {
+                                           const T* __restrict__ Bx, F&& fn,
+                                           const BRec<T>* __restrict__ rec = nullptr) {
     const int nchg = min(TILE_MK, Pb - gb);
     for (int c0 = 0; c0 < nchg; c0 += U * WAVE) {
         IP idx[U];
@@ -113,10 +136,23 @@ __device__ __forceinline__ void walk_group(L& S, int l, int gb, int Pb, int& car
         }
         int col[U];
         T bv[U];
+        if (VALS && rec) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            col[u] = idx[u] >= 0 ? Bj[idx[u]] : -1;
-            bv[u] = (VALS && idx[u] >= 0) ? Bx[idx[u]] : (T)0;
+            for (int u = 0; u < U; ++u) {
+                col[u] = -1;
+                bv[u] = (T)0;
+                if (idx[u] >= 0) {
+                    const BRec<T> r = rec[idx[u]];
+                    col[u] = r.c;
+                    bv[u] = r.v;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                col[u] = idx[u] >= 0 ? Bj[idx[u]] : -1;
+                bv[u] = (VALS && idx[u] >= 0) ? Bx[idx[u]] : (T)0;
+            }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -132,7 +168,7 @@ template <typename IP>
 __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile_sym(
     int64_t row0, int64_t nrows, int tws, int G, int twss, const IP* __restrict__ Ap,
     const int32_t* __restrict__ Aj, const IP* __restrict__ Bp, const int32_t* __restrict__ Bj,
-    const uint32_t* __restrict__ tidx, uint32_t* __restrict__ bitmap, int64_t* __restrict__ item_cnt) {
+    const uint2* __restrict__ tidx, uint32_t* __restrict__ bitmap, int64_t* __restrict__ item_cnt) {
     __shared__ __attribute__((aligned(16))) SymLds<IP> lds[TILE_WPB];
     const int l = lane_id();
     const int wv = uniform((int)(threadIdx.x >> 6));
@@ -166,9 +202,9 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile_sym(
                     cnt = (int)(Bp[k + 1] - rb);
                     beg = rb;
                 } else {
-                    const uint32_t* tk = tidx + (int64_t)k * (G + 1);
-                    const uint32_t s0 = tk[t0];
-                    cnt = (int)(tk[t1] - s0);
+                    const uint2* tk = tidx + (int64_t)k * G;
+                    const uint32_t s0 = tk[t0].x;
+                    cnt = (int)(tk[t1 - 1].y - s0);
                     beg = rb + (IP)s0;
                 }
             }
@@ -201,244 +237,157 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile_sym(
     }
 }
 
-constexpr int TILE_NB = 8;   // batches of A entries kept in registers (rows with <= 512 entries)
-
-// MODE: SHORT_SYM -> bitmap of the item's columns into `bitmap`, its popcount into
-//                    item_cnt[item];
-//       SHORT_NUM -> reads the bitmap back and writes values at Cj/Cx + item_off[item].
-// A wave takes a task = one row and a run of T consecutive tiles [g0, g0 + T): the row's A
-// entries, their B row starts and first tile offsets stay in registers across the run, and
-// a tile's segment ends become the next tile's starts, so each tile costs one index load
-// per A entry (all issued together).
-template <typename T, typename IP, int MODE, bool RUN>
+// Numeric pass of the tile path: one wave per item (row, numeric tile).  Reads the item's
+// bitmap from the symbolic pass, enumerates its products in flattened (jj, kk) order --
+// one 8-byte index load per A entry, one record load per product from the packed B --
+// and accumulates lowest-lane-first per output position; items with more than CAP entries
+// go in column windows (products re-read per window).
+template <typename T, typename IP>
 __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile(
-    int64_t row0, int64_t nrows, int64_t ncols, int tws, int G, int TR,
-    const IP* __restrict__ Ap, const int32_t* __restrict__ Aj, const T* __restrict__ Ax,
-    const IP* __restrict__ Bp, const int32_t* __restrict__ Bj, const T* __restrict__ Bx,
-    const uint32_t* __restrict__ tidx, uint32_t* __restrict__ bitmap, int64_t* __restrict__ item_cnt,
-    const int64_t* __restrict__ item_off, int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha) {
-    constexpr bool VALS = MODE != SHORT_SYM;
+    int64_t row0, int64_t nrows, int tws, int G, const IP* __restrict__ Ap,
+    const int32_t* __restrict__ Aj, const T* __restrict__ Ax, const IP* __restrict__ Bp,
+    const BRec<T>* __restrict__ brec, const uint2* __restrict__ tidx,
+    const uint32_t* __restrict__ bitmap, const int64_t* __restrict__ item_off,
+    int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha) {
     constexpr int U = 8;
-    constexpr int NB = TILE_NB;
-    __shared__ __attribute__((aligned(16))) TileLds<T, IP, VALS> lds[TILE_WPB];
+    __shared__ __attribute__((aligned(16))) TileLds<T, IP, true> lds[TILE_WPB];
     const int l = lane_id();
     const int wv = uniform((int)(threadIdx.x >> 6));
-    TileLds<T, IP, VALS>& S = lds[wv];
+    TileLds<T, IP, true>& S = lds[wv];
     const int TW = 1 << tws;
     const int nw = TW >> 5;                    // bitmap words of a tile
     const int wpl = (nw + WAVE - 1) / WAVE;    // words per lane (<= 2)
-    const int runs = (G + TR - 1) / TR;        // tile runs per row
-    const uint32_t tasks = (uint32_t)(nrows * runs);
-    for (uint32_t task = xcd_block(gridDim.x) * TILE_WPB + wv; task < tasks; task += gridDim.x * TILE_WPB) {
-        const int64_t row = row0 + (int64_t)(task / (uint32_t)runs);
-        const int g0 = (int)(task % (uint32_t)runs) * TR;
-        const int g1 = min(G, g0 + TR);
+    const uint32_t items = (uint32_t)(nrows * G);   // host keeps rows*G < 2^31
+    for (uint32_t it = xcd_block(gridDim.x) * TILE_WPB + wv; it < items; it += gridDim.x * TILE_WPB) {
+        const int64_t row = row0 + (int64_t)(it / (uint32_t)G);
+        const int g = (int)(it % (uint32_t)G);
+        const int64_t item = row * G + g;
+        const int lo = g * TW;
         const int64_t a0 = Ap[row];
         const int nA = (int)(Ap[row + 1] - a0);
-        if (nA <= 0) {
-            if (MODE == SHORT_SYM)
-                for (int g = g0 + l; g < g1; g += WAVE) item_cnt[row * G + g] = 0;
-            continue;
+        if (nA <= 0) continue;
+        const uint32_t* __restrict__ ibits = bitmap + item * nw;
+        // the symbolic bitmap and its popcount prefix (lane owns wpl words)
+        const int w0 = min(nw, l * wpl), w1 = min(nw, w0 + wpl);
+        uint32_t wd[2] = {0u, 0u};
+        int mine = 0;
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+            if (w0 + q < w1) {
+                wd[q] = ibits[w0 + q];
+                mine += __popc(wd[q]);
+            }
+        const int pincl = wave_incl_sum_dpp(mine);
+        const int nnz = readlane_i(pincl, WAVE - 1);
+        if (nnz == 0) continue;
+        const int p0 = pincl - mine;
+        wsync();
+        {
+            int run = p0;
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+                if (w0 + q < w1) {
+                    S.bits[w0 + q] = wd[q];
+                    S.wpre[w0 + q] = (uint16_t)run;
+                    run += __popc(wd[q]);
+                }
         }
-        const bool inreg = RUN && nA <= NB * WAVE;
-        uint32_t tb[NB];   // index row base k * (G + 1); host keeps B.rows * (G + 1) < 2^32
-        IP br[NB];
-        T ar[NB];
-        uint32_t sr[NB], er[NB];
-        if (inreg) {
-            int32_t kr[NB];
-#pragma unroll
-            for (int q = 0; q < NB; ++q) {
-                kr[q] = -1;
-                ar[q] = (T)0;
-                if (q * WAVE < nA && q * WAVE + l < nA) {
-                    kr[q] = Aj[a0 + q * WAVE + l];
-                    if (VALS) ar[q] = Ax[a0 + q * WAVE + l];
-                }
+        wsync();
+        const int64_t obase = item_off[item];
+        // lane info of one batch of A entries: (first B index, count) of its tile segment
+        auto batch = [&](int b, int& cnt, int& off, int& Pb) {
+            cnt = 0;
+            IP beg = 0;
+            T av = (T)0;
+            if (b + l < nA) {
+                const int32_t k = Aj[a0 + b + l];
+                const uint2 se = tidx[(int64_t)k * G + g];
+                cnt = (int)(se.y - se.x);
+                beg = Bp[k] + (IP)se.x;
+                av = Ax[a0 + b + l];
             }
-#pragma unroll
-            for (int q = 0; q < NB; ++q) {
-                br[q] = 0;
-                sr[q] = 0;
-                tb[q] = 0xffffffffu;
-                if (kr[q] >= 0) {
-                    tb[q] = (uint32_t)kr[q] * (uint32_t)(G + 1);
-                    br[q] = Bp[kr[q]];
-                    sr[q] = tidx[tb[q] + (uint32_t)g0];
-                }
-            }
-        }
-        for (int g = g0; g < g1; ++g) {
-            const int64_t item = row * G + g;
-            const int lo = g * TW;
-            uint32_t* __restrict__ ibits = bitmap + item * nw;
-            if (inreg) {
-#pragma unroll
-                for (int q = 0; q < NB; ++q)
-                    er[q] = tb[q] != 0xffffffffu ? tidx[tb[q] + (uint32_t)(g + 1)] : 0u;
-            }
-            // lane info of one batch of A entries: (first B index, count) of its tile segment
-            auto batch = [&](int b, int& cnt, int& off, int& Pb) {
-                cnt = 0;
-                IP beg = 0;
-                T av = (T)0;
-                if (inreg) {
-#pragma unroll
-                    for (int q = 0; q < NB; ++q)
-                        if (q == (b >> 6)) {
-                            cnt = (int)(er[q] - sr[q]);
-                            beg = br[q] + (IP)sr[q];
-                            av = ar[q];
-                        }
-                } else if (b + l < nA) {
-                    const int32_t k = Aj[a0 + b + l];
-                    const uint32_t* tk = tidx + (int64_t)k * (G + 1) + g;
-                    const uint32_t s0 = tk[0];
-                    cnt = (int)(tk[1] - s0);
-                    beg = Bp[k] + (IP)s0;
-                    if (VALS) av = Ax[a0 + b + l];
-                }
-                const int incl = wave_incl_sum_dpp(cnt);
-                off = incl - cnt;
-                Pb = readlane_i(incl, WAVE - 1);
-                wsync();
-                S.jb0[l] = beg;
-                S.joff[l] = (uint32_t)off;
-                if (VALS) S.ja[l] = av;
-                wsync();
-            };
+            const int incl = wave_incl_sum_dpp(cnt);
+            off = incl - cnt;
+            Pb = readlane_i(incl, WAVE - 1);
             wsync();
-            if (MODE == SHORT_SYM) {
-                // ---- structure of the tile -> LDS bitmap -> global bitmap + count
-                for (int w = l; w < nw; w += WAVE) S.bits[w] = 0u;
-                wsync();
-                for (int b = 0; b < nA; b += WAVE) {
-                    int cnt, off, Pb;
-                    batch(b, cnt, off, Pb);
-                    int carry = -1;
-                    for (int gb = 0; gb < Pb; gb += TILE_MK) {
-                        group_markers(S, l, cnt, off, gb);
-                        walk_group<U, false, T, IP>(S, l, gb, Pb, carry, Bj, Bx, [&](int c, T, T) {
-                            if (c >= 0) set_bit(S.bits, c - lo);
-                        });
-                    }
-                }
-                wsync();
-                int mine = 0;
-                for (int w = l; w < nw; w += WAVE) {
-                    const uint32_t x = S.bits[w];
-                    ibits[w] = x;
-                    mine += __popc(x);
-                }
-                const int nnz = readlane_i(wave_incl_sum_dpp(mine), WAVE - 1);
-                if (l == 0) item_cnt[item] = nnz;
-            } else {
-                // ---- numeric: the symbolic bitmap, its popcount prefix (lane owns wpl words)
-                const int w0 = min(nw, l * wpl), w1 = min(nw, w0 + wpl);
-                uint32_t wd[2] = {0u, 0u};
-                int mine = 0;
-#pragma unroll
-                for (int q = 0; q < 2; ++q)
-                    if (w0 + q < w1) {
-                        wd[q] = ibits[w0 + q];
-                        mine += __popc(wd[q]);
-                    }
-                const int pincl = wave_incl_sum_dpp(mine);
-                const int nnz = readlane_i(pincl, WAVE - 1);
-                const int p0 = pincl - mine;
-                if (nnz > 0) {
-                    {
-                        int run = p0;
-#pragma unroll
-                        for (int q = 0; q < 2; ++q)
-                            if (w0 + q < w1) {
-                                S.bits[w0 + q] = wd[q];
-                                S.wpre[w0 + q] = (uint16_t)run;
-                                run += __popc(wd[q]);
-                            }
-                    }
-                    wsync();
-                    const int64_t obase = item_off[item];
-                    // values, per column window of <= CAP entries (whole lanes' words)
-                    for (int L0 = 0; L0 < WAVE;) {
-                        int L1 = WAVE, wb = 0, wn = nnz;
-                        if (nnz > TILE_CAP) {
-                            wb = readlane_i(p0, L0);
-                            L1 = (int)__popcll(__ballot(pincl <= wb + TILE_CAP));
-                            if (L1 <= L0) L1 = L0 + 1;
-                            wn = (L1 < WAVE ? readlane_i(p0, L1) : nnz) - wb;
+            S.jb0[l] = beg;
+            S.joff[l] = (uint32_t)off;
+            S.ja[l] = av;
+            wsync();
+        };
+        for (int L0 = 0; L0 < WAVE;) {
+            int L1 = WAVE, wb = 0, wn = nnz;
+            if (nnz > TILE_CAP) {
+                wb = readlane_i(p0, L0);
+                L1 = (int)__popcll(__ballot(pincl <= wb + TILE_CAP));
+                if (L1 <= L0) L1 = L0 + 1;
+                wn = (L1 < WAVE ? readlane_i(p0, L1) : nnz) - wb;
+            }
+            const int clo = lo + 32 * wpl * L0, chi = lo + 32 * wpl * L1;
+            for (int p = l; p < wn; p += WAVE) {
+                S.acc[p] = (T)0;
+                S.tag[p] = 0xffffffffu;
+            }
+            wsync();
+            uint32_t seq = 0x3ffffffu;
+            for (int b = 0; b < nA; b += WAVE) {
+                int cnt, off, Pb;
+                batch(b, cnt, off, Pb);
+                int carry = -1;
+                for (int gb = 0; gb < Pb; gb += TILE_MK) {
+                    group_markers(S, l, cnt, off, gb);
+                    walk_group<U, true, T, IP>(S, l, gb, Pb, carry, (const int32_t*)nullptr, (const T*)nullptr,
+                                               [&](int c, T bval, T aval) {
+                        int pos = -1;
+                        if (c >= clo && c < chi) {
+                            const int rc = c - lo, w = rc >> 5;
+                            pos = (int)S.wpre[w] + __popc(S.bits[w] & ((1u << (rc & 31)) - 1u)) - wb;
                         }
-                        const int clo = lo + 32 * wpl * L0, chi = lo + 32 * wpl * L1;
-                        for (int p = l; p < wn; p += WAVE) {
-                            S.acc[p] = (T)0;
-                            S.tag[p] = 0xffffffffu;
-                        }
-                        wsync();
-                        uint32_t seq = 0x3ffffffu;
-                        for (int b = 0; b < nA; b += WAVE) {
-                            int cnt, off, Pb;
-                            batch(b, cnt, off, Pb);
-                            int carry = -1;
-                            for (int gb = 0; gb < Pb; gb += TILE_MK) {
-                                group_markers(S, l, cnt, off, gb);
-                                walk_group<U, true, T, IP>(S, l, gb, Pb, carry, Bj, Bx, [&](int c, T bval, T aval) {
-                                    int pos = -1;
-                                    if (c >= clo && c < chi) {
-                                        const int rc = c - lo, w = rc >> 5;
-                                        pos = (int)S.wpre[w] + __popc(S.bits[w] & ((1u << (rc & 31)) - 1u)) - wb;
-                                    }
-                                    const T pv = mul_rn(aval, bval);
-                                    bool pending = pos >= 0;
-                                    while (__ballot(pending)) {
-                                        const uint32_t key = (seq << 6) | (uint32_t)l;
-                                        if (pending) {
-                                            atomicMin(&S.tag[pos], key);
-                                            if (__hip_atomic_load(&S.tag[pos], __ATOMIC_RELAXED,
-                                                                  __HIP_MEMORY_SCOPE_WAVEFRONT) == key) {
-                                                S.acc[pos] = add_rn(S.acc[pos], pv);
-                                                pending = false;
-                                            }
-                                        }
-                                        --seq;
-                                    }
-                                    if (seq < 4096u) {   // re-arm the tag space (very long items only)
-                                        wsync();
-                                        for (int p = l; p < wn; p += WAVE) S.tag[p] = 0xffffffffu;
-                                        seq = 0x3ffffffu;
-                                        wsync();
-                                    }
-                                });
-                            }
-                        }
-                        wsync();
-                        // column list of this window from the bitmap (lane-owned words)
-                        if (l >= L0 && l < L1) {
-                            int p = p0 - wb;
-                            for (int w = w0; w < w1; ++w) {
-                                uint32_t x = S.bits[w];
-                                while (x) {
-                                    S.tag[p++] = (uint32_t)(lo + 32 * w + __builtin_ctz(x));
-                                    x &= x - 1u;
+                        const T pv = mul_rn(aval, bval);
+                        bool pending = pos >= 0;
+                        while (__ballot(pending)) {
+                            const uint32_t key = (seq << 6) | (uint32_t)l;
+                            if (pending) {
+                                atomicMin(&S.tag[pos], key);
+                                if (__hip_atomic_load(&S.tag[pos], __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_WAVEFRONT) == key) {
+                                    S.acc[pos] = add_rn(S.acc[pos], pv);
+                                    pending = false;
                                 }
                             }
+                            --seq;
                         }
-                        wsync();
-                        int32_t* __restrict__ crow = Cj + obase + wb;
-                        T* __restrict__ xrow = Cx + obase + wb;
-                        for (int p = l; p < wn; p += WAVE) {
-                            crow[p] = (int32_t)S.tag[p];
-                            const T val = S.acc[p];
-                            xrow[p] = (alpha == (T)1) ? val : mul_rn(alpha, val);
+                        if (seq < 4096u) {   // re-arm the tag space (very long items only)
+                            wsync();
+                            for (int p = l; p < wn; p += WAVE) S.tag[p] = 0xffffffffu;
+                            seq = 0x3ffffffu;
+                            wsync();
                         }
-                        wsync();
-                        L0 = L1;
+                    }, brec);
+                }
+            }
+            wsync();
+            // column list of this window from the bitmap (lane-owned words)
+            if (l >= L0 && l < L1) {
+                int p = p0 - wb;
+                for (int w = w0; w < w1; ++w) {
+                    uint32_t x = S.bits[w];
+                    while (x) {
+                        S.tag[p++] = (uint32_t)(lo + 32 * w + __builtin_ctz(x));
+                        x &= x - 1u;
                     }
                 }
             }
-            if (inreg) {
-#pragma unroll
-                for (int q = 0; q < NB; ++q) sr[q] = er[q];
+            wsync();
+            int32_t* __restrict__ crow = Cj + obase + wb;
+            T* __restrict__ xrow = Cx + obase + wb;
+            for (int p = l; p < wn; p += WAVE) {
+                crow[p] = (int32_t)S.tag[p];
+                const T val = S.acc[p];
+                xrow[p] = (alpha == (T)1) ? val : mul_rn(alpha, val);
             }
+            wsync();
+            L0 = L1;
         }
     }
 }
