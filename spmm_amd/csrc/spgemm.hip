@@ -73,6 +73,7 @@ struct spg_plan_s {
     bool fused_failed = false;      // the single pass met a row it cannot take
     bool scaled_in_place = false;   // spg_numeric scaled the workspace result by alpha
     int64_t sym_spills = -1;        // rows the symbolic short-row pass spilled (-1 unknown)
+    int64_t cap = 0;                // ALG1 single pass: entries tj/tx hold (an estimate)
     uint2* tidx = nullptr;          // B column-tile index, B.rows * G (start, end) pairs
     void* brec = nullptr;           // B packed as (column, value) records (numeric tile pass)
     bool brec_built = false;
@@ -329,9 +330,11 @@ Layout make_layout(const spg_plan_s& p) {
         L.bitmap = off; off = align_up(off + sizeof(uint32_t) * (size_t)tile_items(p) * (size_t)((1 << p.tws) >> 5));
     }
     if (p.alg == SPG_ALG1 && !p.use_tile) {
-        L.ub = off; off = align_up(off + sizeof(int64_t) * (size_t)(p.A.rows + 1));
-        L.tj = off; off = align_up(off + sizeof(int32_t) * (size_t)std::max<int64_t>(p.P, 1));
-        L.tx = off; off = align_up(off + vbytes(p.A.value_type) * (size_t)std::max<int64_t>(p.P, 1));
+        // single pass: C itself, `cap` entries (an estimate); upper-bound path: P entries
+        const int64_t n = fused_alg1(p) ? p.cap : p.P;
+        if (!fused_alg1(p)) { L.ub = off; off = align_up(off + sizeof(int64_t) * (size_t)(p.A.rows + 1)); }
+        L.tj = off; off = align_up(off + sizeof(int32_t) * (size_t)std::max<int64_t>(n, 1));
+        L.tx = off; off = align_up(off + vbytes(p.A.value_type) * (size_t)std::max<int64_t>(n, 1));
     }
     L.total = off;
     return L;
@@ -351,7 +354,7 @@ void carve(spg_plan_s& p, const Layout& L) {
         p.bitmap = (uint32_t*)(p.ws + L.bitmap);
     }
     if (p.alg == SPG_ALG1 && !p.use_tile) {
-        p.ub = (int64_t*)(p.ws + L.ub);
+        if (!fused_alg1(p)) p.ub = (int64_t*)(p.ws + L.ub);
         p.tj = (int32_t*)(p.ws + L.tj);
         p.tx = (void*)(p.ws + L.tx);
     }
@@ -444,7 +447,7 @@ spg_status_t run_symbolic_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_
                                (const double*)nullptr, (const int64_t*)nullptr, (int32_t*)nullptr,
                                (double*)nullptr, 1.0, p.row_cnt, l1, cnt, (const int32_t*)nullptr,
                                (const int32_t*)nullptr, (unsigned long long*)nullptr, (int64_t*)nullptr,
-                               (int64_t*)nullptr);
+                               (int64_t*)nullptr, (int64_t)0);
             SPG_LAUNCHED(h);
         }
         PhaseTimer ps(h, SPG_PHASE_SPILL);
@@ -494,7 +497,7 @@ spg_status_t run_numeric_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_t
                                dim3(ShortSmall::WPB * WAVE), 0, h->stream, r0, n, p.B.cols, Ap, Aj, Ax, Bp, Bj,
                                Bx, off, cj, cx, alpha, p.row_cnt, l1, cnt, (const int32_t*)nullptr,
                                (const int32_t*)nullptr, (unsigned long long*)nullptr, (OFF*)nullptr,
-                               (int64_t*)nullptr);
+                               (int64_t*)nullptr, (int64_t)0);
             SPG_LAUNCHED(h);
         }
         if (p.sym_spills == 0) return SPG_STATUS_SUCCESS;
@@ -545,7 +548,7 @@ spg_status_t alg1_fused_run(spg_handle_t h, spg_plan_s& p, void* cp) {
                        (const IP*)p.B.indptr, (const int32_t*)p.B.indices, (const T*)p.B.values,
                        (const OUT*)nullptr, p.tj, (T*)p.tx, (T)1, p.row_cnt, (int32_t*)nullptr,
                        (int32_t*)nullptr, (const int32_t*)nullptr, (const int32_t*)nullptr, p.lb, (OUT*)cp,
-                       p.scalars);
+                       p.scalars, p.cap);
     SPG_LAUNCHED(h);
     return SPG_STATUS_SUCCESS;
 }
@@ -596,7 +599,7 @@ spg_status_t numeric_typed(spg_handle_t h, spg_plan_s& p, const spg_csr_t& C, T 
         }
         return SPG_STATUS_SUCCESS;
     }
-    if (p.alg == SPG_ALG1 && !p.use_tile) {
+    if (p.alg == SPG_ALG1 && !p.use_tile && !fused_alg1(p)) {
         if (p.A.rows > 0) {
             PhaseTimer pt(h, SPG_PHASE_COMPACT);
             hipLaunchKernelGGL((k_compact<T, IPC>), dim3((unsigned)grid_for(p.A.rows, WPB)), dim3(BLOCK), 0,
@@ -743,7 +746,14 @@ spg_status_t spg_plan(spg_handle_t h, const spg_csr_t* A, const spg_csr_t* B, sp
     const bool same_as_query = h->q_valid && h->q_alg == tmp.alg && h->q_cf == chunk_fraction &&
                                std::memcmp(&h->q_A, A, sizeof(spg_csr_t)) == 0 &&
                                std::memcmp(&h->q_B, B, sizeof(spg_csr_t)) == 0;
-    if (tmp.alg == SPG_ALG1 && !tmp.use_tile) {
+    if (fused_alg1(tmp)) {
+        // single pass: the output buffer is sized from the expected product count (no device
+        // pass, no sync); a product that outgrows it is redone two-phase by spg_symbolic
+        const double avgB = B->rows > 0 ? (double)B->nnz / (double)B->rows : 0.0;
+        const double est = 1.15 * (double)A->nnz * avgB + 4096.0;
+        const double full = (double)A->rows * (double)B->cols;
+        tmp.cap = (int64_t)std::min(est, full);
+    } else if (tmp.alg == SPG_ALG1 && !tmp.use_tile) {
         if (workspace && same_as_query) {
             tmp.P = h->q_P;
         } else if ((st = products_total(h, *A, *B, &tmp.P))) {
@@ -844,9 +854,9 @@ spg_status_t spg_symbolic(spg_handle_t h, spg_plan_t p, void* C_indptr, spg_inde
             }
         }
         if (st) return st;
-        int64_t sc[10];
-        if ((st = read_scalars(h, p->scalars, 10, sc))) return st;
-        if (!sc[LB_FAIL]) {
+        int64_t sc[11];
+        if ((st = read_scalars(h, p->scalars, 11, sc))) return st;
+        if (!sc[LB_FAIL] && !sc[LB_CAPX]) {
             p->counts_ready = true;
             p->alg1_fused = true;
             const int64_t tot = sc[LB_TOTAL];
@@ -857,11 +867,10 @@ spg_status_t spg_symbolic(spg_handle_t h, spg_plan_t p, void* C_indptr, spg_inde
             *nnzC = tot;
             return SPG_STATUS_SUCCESS;
         }
-        // a row the single pass cannot take: run the upper-bound path instead
+        // a row the single pass cannot take, or an output larger than the estimate: redo
+        // the product two-phase (symbolic + scan here, numeric straight into C)
         p->fused_failed = true;
         p->symbolic_runs = 0;
-        if ((st = products_prefix(h, p->A, p->B, p->row_cnt, p->ub, p->scalars + 2, p->scan_status, false)))
-            return st;
     }
     if (p->symbolic_runs++ > 0 && !p->use_tile) {
         // a repeated call (e.g. retrying with int64 row pointers): the row counts are kept;
@@ -870,7 +879,7 @@ spg_status_t spg_symbolic(spg_handle_t h, spg_plan_t p, void* C_indptr, spg_inde
         SPG_HIP(h, hipMemsetAsync(p->scan_status + tiles, 0, sizeof(unsigned long long) * tiles, h->stream));
     }
     if (!p->counts_ready) {
-        if (p->alg == SPG_ALG1 && !p->use_tile) {
+        if (p->alg == SPG_ALG1 && !p->use_tile && !fused_alg1(*p)) {
             if (f64)
                 st = i64 ? alg1_compute<double, int64_t>(h, *p) : alg1_compute<double, int32_t>(h, *p);
             else
@@ -887,7 +896,7 @@ spg_status_t spg_symbolic(spg_handle_t h, spg_plan_t p, void* C_indptr, spg_inde
     if ((st = read_scalars(h, p->scalars, 5, sc))) return st;
     // the short-row kernel spills the same rows in both passes: none in the symbolic pass
     // (one launch over all rows) means the numeric spill launch can be skipped
-    if (p->use_short && p->alg == SPG_ALG2) p->sym_spills = (int64_t)(uint32_t)(sc[4] & 0xffffffffu);
+    if (p->use_short && (p->alg == SPG_ALG2 || fused_alg1(*p))) p->sym_spills = (int64_t)(uint32_t)(sc[4] & 0xffffffffu);
     p->counts_ready = true;      // counts (and tile offsets) stay valid for a repeated call
     if (sc[1] || (p->use_tile && C_indptr_type == SPG_INDEX_32I && sc[0] > 2147483647LL))
         return SPG_STATUS_OVERFLOW;

@@ -319,13 +319,13 @@ __global__ __launch_bounds__(BLOCK) void k_numeric(
 // the limits are appended to `spill` (handled by the next kernel; the list order does not
 // affect any result).  Rows come from [row0, row0 + nrows) or, with `list`, from
 // list[0 .. *list_count).
-// SHORT_NUMLB (ALG1 single pass): one wave per row in row order; each row publishes its entry
-// count, looks back over its predecessors for its exclusive offset (decoupled look-back, as
-// k_scan_lb) and writes its columns and values straight to their final place and its row
-// pointer to Cp.  A row the kernel cannot take sets scal[LB_FAIL] (the host then runs the
-// SHORT_NUMUB path); it still publishes, so no successor waits forever.
+// SHORT_NUMLB (ALG1 single pass): one wave per row, rows in dispatch order.  The rows of a
+// block share one decoupled look-back (see lb_lead): each row gets its offset and writes its
+// columns and values straight into Cj/Cx -- at most `cap` entries; a row past that sets
+// scal[LB_CAPX] and writes nothing -- and its row pointer into Cp.  A row this kernel cannot
+// take sets scal[LB_FAIL].  Either flag makes the host redo the product two-phase.
 enum { SHORT_SYM = 0, SHORT_NUM = 1, SHORT_NUMUB = 2, SHORT_NUMLB = 3 };
-enum { LB_TICKET = 6, LB_FAIL = 7, LB_TOTAL = 8, LB_OVERFLOW = 9 };
+enum { LB_TICKET = 6, LB_FAIL = 7, LB_TOTAL = 8, LB_OVERFLOW = 9, LB_CAPX = 10 };
 
 // Block `row` publishes its aggregate (flag 1) or, for block 0, its inclusive prefix (flag 2).
 __device__ __forceinline__ void lb_publish(unsigned long long* st, int64_t row, int64_t v, int l) {
@@ -419,7 +419,7 @@ __global__ __launch_bounds__(G::WPB * WAVE, 5) void k_short(
     int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha, int64_t* __restrict__ row_cnt,
     int32_t* __restrict__ spill, int32_t* __restrict__ spill_count,
     const int32_t* __restrict__ list, const int32_t* __restrict__ list_count,
-    unsigned long long* __restrict__ lb, OFF* __restrict__ Cp, int64_t* __restrict__ scal) {
+    unsigned long long* __restrict__ lb, OFF* __restrict__ Cp, int64_t* __restrict__ scal, int64_t cap) {
     constexpr int R = G::R;
     constexpr bool LB = MODE == SHORT_NUMLB;
     constexpr bool VALS = MODE != SHORT_SYM;
@@ -707,11 +707,15 @@ __global__ __launch_bounds__(G::WPB * WAVE, 5) void k_short(
                 }
             }
             wsync();
-            if (LB && cbase < 0) cbase = lb_row_base(row, nnz);
+            if (LB && cbase < 0) {
+                cbase = lb_row_base(row, nnz);
+                if (cbase + nnz > cap && l == 0) scal[LB_CAPX] = 1;   // output buffer too small
+            }
             const int64_t rbase = LB ? cbase : (int64_t)Coff[row];
             int32_t* __restrict__ crow = Cj + rbase + wb;
             T* __restrict__ xrow = Cx + rbase + wb;
-            for (int p = l; p < wn; p += WAVE) {
+            const int wlim = (LB && cbase + nnz > cap) ? 0 : wn;
+            for (int p = l; p < wlim; p += WAVE) {
                 crow[p] = (int32_t)S.tag[p];
                 const T val = S.acc[p];
                 xrow[p] = (alpha == (T)1) ? val : mul_rn(alpha, val);

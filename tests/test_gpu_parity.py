@@ -376,3 +376,24 @@ def test_alg1_single_pass_abi_sequence():
         torch.cuda.synchronize()
         _assert_same((p64.cpu().numpy(), cj.cpu().numpy(), cx.cpu().numpy()), ref)
         lib.spg_plan_destroy(plan)
+
+
+def test_alg1_single_pass_estimate_overflow():
+    """ALG1's single pass sizes its output from the expected product count; when A's
+    entries select B's longest rows, the output outgrows the estimate and the product is
+    redone two-phase, with the same bits."""
+    rng = np.random.default_rng(43)
+    B = sp.random(2000, 3000, density=0.001, format="lil", random_state=rng)
+    for r in range(10):
+        B[r, rng.choice(3000, 1500, replace=False)] = rng.standard_normal(1500)
+    B = sp.csr_matrix(B)
+    rows, cols = [], []
+    for i in range(3000):
+        for c in rng.choice(10, 5, replace=False):
+            rows.append(i); cols.append(c)
+    A = sp.csr_matrix((rng.standard_normal(len(rows)), (rows, cols)), shape=(3000, 2000))
+    for M in (A, B):
+        M.sum_duplicates(); M.sort_indices()
+    ref = oracle.spgemm(A, B, alpha=1.5, keep_zeros=True, sort=True)
+    assert len(ref[1]) > 10 * A.nnz * (B.nnz / B.shape[0])
+    _assert_same(_gpu(A, B, alg=1, alpha=1.5), ref)
