@@ -31,6 +31,21 @@ template <typename T, typename IP, bool VALS> struct TileLds {
     int8_t mk[TILE_MK];
 };
 
+// Numeric tile pass LDS: the bitmap word and its popcount prefix side by side (one 8-byte
+// read per product), the A-entry table as one 16-byte entry per lane.
+template <typename T, typename IP> struct __attribute__((aligned(16))) TileEnt {
+    IP jb0;          // first B index of the entry's segment
+    uint32_t joff;   // flattened offset of the segment's first product
+    T ja;            // the A value
+};
+template <typename T, typename IP> struct NumLds {
+    uint2 bw[TILE_NWMAX];   // (bitmap word, popcount prefix)
+    T acc[TILE_CAP];
+    uint32_t tag[TILE_CAP];
+    TileEnt<T, IP> ent[WAVE];
+    int8_t mk[TILE_MK];
+};
+
 // ---------------------------------------------------------------------------------------
 // B column-tile index: tidx[k*G + g] = (start, end) of B row k's entries with columns in
 // tile g, as offsets inside the row (one 8-byte load per segment).  start_g = first entry
@@ -67,6 +82,20 @@ __global__ __launch_bounds__(256) void k_tile_index(int64_t rows, const IP* __re
 template <typename T> struct BRec;
 template <> struct __attribute__((aligned(16))) BRec<double> { int32_t c; int32_t pad; double v; };
 template <> struct __attribute__((aligned(8))) BRec<float> { int32_t c; float v; };
+
+// One load per record: 16 bytes (f64) or 8 bytes (f32).
+template <typename T, typename IP>
+__device__ __forceinline__ void load_rec(const BRec<T>* __restrict__ rec, IP i, int& c, T& v) {
+    if constexpr (sizeof(T) == 8) {
+        const uint4 q = reinterpret_cast<const uint4*>(rec)[i];
+        c = (int)q.x;
+        v = __hiloint2double((int)q.w, (int)q.z);
+    } else {
+        const uint2 q = reinterpret_cast<const uint2*>(rec)[i];
+        c = (int)q.x;
+        v = __uint_as_float(q.y);
+    }
+}
 
 template <typename T>
 __global__ __launch_bounds__(256) void k_pack_b(int64_t nnz, const int32_t* __restrict__ Bj,
@@ -250,10 +279,10 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile(
     const uint32_t* __restrict__ bitmap, const int64_t* __restrict__ item_off,
     int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha) {
     constexpr int U = 8;
-    __shared__ __attribute__((aligned(16))) TileLds<T, IP, true> lds[TILE_WPB];
+    __shared__ __attribute__((aligned(16))) NumLds<T, IP> lds[TILE_WPB];
     const int l = lane_id();
     const int wv = uniform((int)(threadIdx.x >> 6));
-    TileLds<T, IP, true>& S = lds[wv];
+    NumLds<T, IP>& S = lds[wv];
     const int TW = 1 << tws;
     const int nw = TW >> 5;                    // bitmap words of a tile
     const int wpl = (nw + WAVE - 1) / WAVE;    // words per lane (<= 2)
@@ -287,19 +316,52 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile(
 #pragma unroll
             for (int q = 0; q < 2; ++q)
                 if (w0 + q < w1) {
-                    S.bits[w0 + q] = wd[q];
-                    S.wpre[w0 + q] = (uint16_t)run;
+                    S.bw[w0 + q] = make_uint2(wd[q], (uint32_t)run);
                     run += __popc(wd[q]);
                 }
         }
         wsync();
         const int64_t obase = item_off[item];
+        // The first NB batches of A entries (rows of <= NB*64 entries: all of them): every
+        // lane's A entry, value, tile segment and B row start, loaded at once up front (two
+        // dependent load levels per item instead of two per batch).
+        constexpr int NB = 8;
+        int32_t kq[NB];
+        T aq[NB];
+        uint2 sq[NB];
+        IP bq[NB];
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+            kq[q] = -1;
+            aq[q] = (T)0;
+            if (q * WAVE < nA && q * WAVE + l < nA) {
+                kq[q] = Aj[a0 + q * WAVE + l];
+                aq[q] = Ax[a0 + q * WAVE + l];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+            sq[q] = make_uint2(0u, 0u);
+            bq[q] = 0;
+            if (kq[q] >= 0) {
+                sq[q] = tidx[(int64_t)kq[q] * G + g];
+                bq[q] = Bp[kq[q]];
+            }
+        }
         // lane info of one batch of A entries: (first B index, count) of its tile segment
         auto batch = [&](int b, int& cnt, int& off, int& Pb) {
             cnt = 0;
             IP beg = 0;
             T av = (T)0;
-            if (b + l < nA) {
+            if (b < NB * WAVE) {
+#pragma unroll
+                for (int q = 0; q < NB; ++q)
+                    if (q == (b >> 6)) {
+                        cnt = (int)(sq[q].y - sq[q].x);
+                        beg = bq[q] + (IP)sq[q].x;
+                        av = aq[q];
+                    }
+            } else if (b + l < nA) {
                 const int32_t k = Aj[a0 + b + l];
                 const uint2 se = tidx[(int64_t)k * G + g];
                 cnt = (int)(se.y - se.x);
@@ -310,9 +372,7 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile(
             off = incl - cnt;
             Pb = readlane_i(incl, WAVE - 1);
             wsync();
-            S.jb0[l] = beg;
-            S.joff[l] = (uint32_t)off;
-            S.ja[l] = av;
+            S.ent[l] = TileEnt<T, IP>{beg, (uint32_t)off, av};
             wsync();
         };
         for (int L0 = 0; L0 < WAVE;) {
@@ -329,41 +389,77 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile(
                 S.tag[p] = 0xffffffffu;
             }
             wsync();
-            uint32_t seq = 0x3ffffffu;
+            uint32_t seq = 0x7fffffu;   // 23 bits: key = seq | chunk (3 bits) | lane (6 bits)
             for (int b = 0; b < nA; b += WAVE) {
                 int cnt, off, Pb;
                 batch(b, cnt, off, Pb);
                 int carry = -1;
                 for (int gb = 0; gb < Pb; gb += TILE_MK) {
                     group_markers(S, l, cnt, off, gb);
-                    walk_group<U, true, T, IP>(S, l, gb, Pb, carry, (const int32_t*)nullptr, (const T*)nullptr,
-                                               [&](int c, T bval, T aval) {
-                        int pos = -1;
-                        if (c >= clo && c < chi) {
-                            const int rc = c - lo, w = rc >> 5;
-                            pos = (int)S.wpre[w] + __popc(S.bits[w] & ((1u << (rc & 31)) - 1u)) - wb;
+                    const int nchg = min(TILE_MK, Pb - gb);
+                    for (int c0 = 0; c0 < nchg; c0 += U * WAVE) {
+                        // lane -> A entry of U chunks at once; chunks past the group read the
+                        // -1 markers, so `carry` passes through them unchanged.  Indices of
+                        // lanes past the group are clamped to 0 and their results dropped.
+                        IP idx[U];
+                        T av[U];
+                        bool val[U];
+#pragma unroll
+                        for (int u = 0; u < U; ++u) {
+                            const int cc = c0 + u * WAVE;
+                            const int src = max(wave_incl_max_dpp((int)S.mk[cc + l]), carry);
+                            carry = readlane_i(src, WAVE - 1);
+                            const int t = gb + cc + l;
+                            val[u] = t < Pb;
+                            const TileEnt<T, IP> e = S.ent[max(src, 0)];
+                            idx[u] = val[u] ? e.jb0 + (IP)(t - (int)e.joff) : (IP)0;
+                            av[u] = e.ja;
                         }
-                        const T pv = mul_rn(aval, bval);
-                        bool pending = pos >= 0;
-                        while (__ballot(pending)) {
-                            const uint32_t key = (seq << 6) | (uint32_t)l;
-                            if (pending) {
-                                atomicMin(&S.tag[pos], key);
-                                if (__hip_atomic_load(&S.tag[pos], __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_WAVEFRONT) == key) {
-                                    S.acc[pos] = add_rn(S.acc[pos], pv);
-                                    pending = false;
-                                }
+                        int qc[U];
+                        T qv[U];
+#pragma unroll
+                        for (int u = 0; u < U; ++u) load_rec(brec, idx[u], qc[u], qv[u]);
+                        // positions and products of all U chunks, then one joint owner
+                        // round for the U*64 products: key (seq, chunk, lane) orders them by
+                        // flattened index, so the lowest pending product of every position
+                        // adds first; a lane's U atomics are independent and pipeline
+                        int pos[U];
+                        T pv[U];
+                        uint32_t pend = 0u;
+#pragma unroll
+                        for (int u = 0; u < U; ++u) {
+                            const int c = (val[u] && c0 + u * WAVE < nchg) ? qc[u] : -1;
+                            pos[u] = 0;
+                            if (c >= clo && c < chi) {
+                                const int rc = c - lo;
+                                const uint2 bw = S.bw[rc >> 5];
+                                pos[u] = (int)bw.y + __popc(bw.x & ((1u << (rc & 31)) - 1u)) - wb;
+                                pend |= 1u << u;
                             }
+                            pv[u] = mul_rn(av[u], qv[u]);
+                        }
+                        while (__ballot(pend != 0u)) {
+                            const uint32_t kb = (seq << 9) | (uint32_t)l;
+#pragma unroll
+                            for (int u = 0; u < U; ++u)
+                                if (pend & (1u << u)) atomicMin(&S.tag[pos[u]], kb | ((uint32_t)u << 6));
+#pragma unroll
+                            for (int u = 0; u < U; ++u)
+                                if ((pend & (1u << u)) &&
+                                    __hip_atomic_load(&S.tag[pos[u]], __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_WAVEFRONT) == (kb | ((uint32_t)u << 6))) {
+                                    S.acc[pos[u]] = add_rn(S.acc[pos[u]], pv[u]);
+                                    pend &= ~(1u << u);
+                                }
                             --seq;
                         }
                         if (seq < 4096u) {   // re-arm the tag space (very long items only)
                             wsync();
                             for (int p = l; p < wn; p += WAVE) S.tag[p] = 0xffffffffu;
-                            seq = 0x3ffffffu;
+                            seq = 0x7fffffu;
                             wsync();
                         }
-                    }, brec);
+                    }
                 }
             }
             wsync();
@@ -371,7 +467,7 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile(
             if (l >= L0 && l < L1) {
                 int p = p0 - wb;
                 for (int w = w0; w < w1; ++w) {
-                    uint32_t x = S.bits[w];
+                    uint32_t x = S.bw[w].x;
                     while (x) {
                         S.tag[p++] = (uint32_t)(lo + 32 * w + __builtin_ctz(x));
                         x &= x - 1u;
