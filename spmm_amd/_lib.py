@@ -18,7 +18,7 @@ import threading
 import torch  # noqa: F401  (must be loaded before the HIP library, see module doc)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libmi355_spgemm.so")
+LIB_PATH = os.environ.get("SPG_LIB") or os.path.join(_HERE, "lib", "libmi355_spgemm.so")   # SPG_LIB: an alternative build (A/B timing)
 
 # enums of include/spgemm.h
 SPG_INDEX_32I = 32
@@ -98,6 +98,7 @@ def load():
             "spg_plan": (ctypes.c_int, [vp, csrp, csrp, ctypes.c_int, ctypes.c_float,
                                         ctypes.POINTER(sz), vp, ctypes.POINTER(vp)]),
             "spg_num_products": (ctypes.c_int, [vp, vp, ctypes.POINTER(i64)]),
+            "spg_result_in_workspace": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp)]),
             "spg_symbolic": (ctypes.c_int, [vp, vp, vp, ctypes.c_int, ctypes.POINTER(i64)]),
             "spg_numeric": (ctypes.c_int, [vp, vp, vp, csrp]),
             "spg_peak_bytes": (ctypes.c_int, [vp, ctypes.POINTER(sz)]),
