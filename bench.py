@@ -198,6 +198,16 @@ def main():
             _ = A_h @ B_h
             st.append(time.perf_counter() - t0)
         t_scipy = float(np.median(st))
+        # multi-core point: the same restatement with OpenMP over rows on the host cores
+        # (OMP_NUM_THREADS when set -- 16 on the GPU box -- else every visible core)
+        nthr = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+        om = []
+        t_start = time.perf_counter()
+        while len(om) < 20 and (len(om) < 3 or time.perf_counter() - t_start < args.cpu_seconds / 2):
+            t0 = time.perf_counter()
+            oracle.spgemm(A_h, B_h, keep_zeros=True, sort=True, threads=nthr)
+            om.append(time.perf_counter() - t0)
+        t_omp = float(np.median(om))
         cpu = {"value": round(2.0 * P / t_port / 1e9, 4), "unit": "GFLOPS", "cores": 1,
                "kind": "port",
                "sample": f"full config product (same A,B), median of {len(times)} runs, "
@@ -205,6 +215,9 @@ def main():
                "ms_per_step": round(t_port * 1e3, 3),
                "scipy_ms": round(t_scipy * 1e3, 3),
                "scipy_gflops": round(2.0 * P / t_scipy / 1e9, 4),
+               "omp": {"threads": nthr, "ms_per_step": round(t_omp * 1e3, 3),
+                       "gflops": round(2.0 * P / t_omp / 1e9, 4),
+                       "sample": f"oracle/gustavson.c OpenMP over rows, median of {len(om)} runs"},
                "host_cpus": os.cpu_count()}
 
     if rank == 0:

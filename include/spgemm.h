@@ -73,8 +73,10 @@ typedef enum {
 /* Index type of a row pointer (indptr).  Column indices are always int32. */
 typedef enum { SPG_INDEX_32I = 32, SPG_INDEX_64I = 64 } spg_index_t;
 
-/* Value type.  Numbers equal cudaDataType's CUDA_R_32F / CUDA_R_64F. */
-typedef enum { SPG_R_32F = 0, SPG_R_64F = 1 } spg_dtype_t;
+/* Value type.  Numbers equal cudaDataType's CUDA_R_32F / CUDA_R_64F / CUDA_C_32F /
+ * CUDA_C_64F (cupyx/cusparse.py takes f32/f64/c64/c128, test_cusparse.py:372-375).
+ * Complex values are (real, imag) pairs, numpy's layout; alpha then points to one pair. */
+typedef enum { SPG_R_32F = 0, SPG_R_64F = 1, SPG_C_32F = 4, SPG_C_64F = 5 } spg_dtype_t;
 
 /* Algorithm selector (cusparseSpGEMMAlg_t roles, cupy-src/cupy_backends/cuda/libs/
  * cusparse.pxd:158-164; chosen at cupy-src/cupyx/cusparse.py:2052-2057):

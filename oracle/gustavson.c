@@ -39,6 +39,30 @@
 #include <omp.h>
 #endif
 
+/* Value types.  Complex values follow scipy's sparsetools `complex_wrapper` (and numpy's
+ * complex multiply for alpha * C): (a+bi)(c+di) = (ac - bd) + (ad + bc)i with every
+ * product and every sum rounded on its own; a sum is "zero" when both parts are 0. */
+typedef struct { float re, im; } orc_c64;
+typedef struct { double re, im; } orc_c128;
+
+#define REAL_OPS(T, SUF)                                                                    \
+    static inline T mul_##SUF(T a, T b) { return a * b; }                                   \
+    static inline T add_##SUF(T a, T b) { return a + b; }                                   \
+    static inline int nz_##SUF(T a) { return a != 0; }                                      \
+    static inline int one_##SUF(T a) { return a == (T)1; }                                  \
+    static inline T zero_##SUF(void) { return (T)0; }
+#define CPLX_OPS(T, SUF)                                                                    \
+    static inline T mul_##SUF(T a, T b) {                                                   \
+        T r; r.re = a.re * b.re - a.im * b.im; r.im = a.re * b.im + a.im * b.re; return r; } \
+    static inline T add_##SUF(T a, T b) { T r; r.re = a.re + b.re; r.im = a.im + b.im; return r; } \
+    static inline int nz_##SUF(T a) { return a.re != 0 || a.im != 0; }                     \
+    static inline int one_##SUF(T a) { return a.re == 1 && a.im == 0; }                     \
+    static inline T zero_##SUF(void) { T r; r.re = 0; r.im = 0; return r; }
+REAL_OPS(float, f32)
+REAL_OPS(double, f64)
+CPLX_OPS(orc_c64, c64)
+CPLX_OPS(orc_c128, c128)
+
 /* P = number of scalar products = sum over A entries of nnz(B row) (cusparseSpGEMM_getNumProducts). */
 int64_t orc_num_products(int64_t n_row, const int64_t *Ap, const int32_t *Aj, const int64_t *Bp)
 {
@@ -116,21 +140,21 @@ int64_t orc_symbolic(int64_t n_row, int64_t n_col, const int64_t *Ap, const int3
             T v = Ax[jj];                                                                   \
             for (int64_t kk = Bp[j]; kk < Bp[j + 1]; ++kk) {                                \
                 int32_t k = Bj[kk];                                                         \
-                T prod = v * Bx[kk];                                                        \
-                sums[k] = sums[k] + prod;                                                   \
+                T prod = mul_##SUF(v, Bx[kk]);                                              \
+                sums[k] = add_##SUF(sums[k], prod);                                         \
                 if (next[k] == -1) { next[k] = head; head = k; ++length; }                  \
             }                                                                               \
         }                                                                                   \
         for (int64_t q = 0; q < length; ++q) {                                              \
-            if (keep_zeros || sums[head] != 0) {                                            \
+            if (keep_zeros || nz_##SUF(sums[head])) {                                       \
                 Cj[w] = (int32_t)head;                                                      \
-                Cx[w] = (alpha == (T)1) ? sums[head] : alpha * sums[head];                  \
+                Cx[w] = one_##SUF(alpha) ? sums[head] : mul_##SUF(alpha, sums[head]);       \
                 ++w;                                                                        \
             }                                                                               \
             int64_t tmp = head;                                                             \
             head = next[head];                                                              \
             next[tmp] = -1;                                                                 \
-            sums[tmp] = 0;                                                                  \
+            sums[tmp] = zero_##SUF();                                                       \
         }                                                                                   \
         return w;                                                                           \
     }
@@ -203,6 +227,8 @@ int64_t orc_symbolic(int64_t n_row, int64_t n_col, const int64_t *Ap, const int3
 
 DEFINE_SPGEMM(double, f64)
 DEFINE_SPGEMM(float, f32)
+DEFINE_SPGEMM(orc_c64, c64)
+DEFINE_SPGEMM(orc_c128, c128)
 
 /* Canonical-format check (restates cupyx _has_canonical_format_kern,
  * modify_src/cupy-src/cupyx/scipy/sparse/_compressed.py:177-192): indptr non-decreasing

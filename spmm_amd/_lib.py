@@ -25,6 +25,8 @@ SPG_INDEX_32I = 32
 SPG_INDEX_64I = 64
 SPG_R_32F = 0
 SPG_R_64F = 1
+SPG_C_32F = 4
+SPG_C_64F = 5
 SPG_ALG_DEFAULT, SPG_ALG1, SPG_ALG2, SPG_ALG3 = 0, 1, 2, 3
 
 STATUS_NAMES = {

@@ -30,6 +30,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace spg {
 
 constexpr int WAVE = 64;
@@ -111,12 +113,47 @@ __device__ __forceinline__ int wave_incl_max_dpp(int v) {
 
 __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// Complex values (complex64 / complex128): two parts side by side, numpy's layout.  The
+// default constructor is trivial, so the type can live in __shared__ arrays.
+template <typename R> struct cplx {
+    R re, im;
+    cplx() = default;
+    __host__ __device__ constexpr cplx(R r, R i) : re(r), im(i) {}
+    __host__ __device__ constexpr cplx(int r) : re(R(r)), im(R(0)) {}   // (T)0, (T)1
+};
+template <typename R> __host__ __device__ inline bool operator==(cplx<R> a, cplx<R> b) {
+    return a.re == b.re && a.im == b.im;
+}
+template <typename R> __host__ __device__ inline bool operator!=(cplx<R> a, cplx<R> b) { return !(a == b); }
+
+// Separately rounded multiply and add (no contraction into FMA).  Complex products follow
+// scipy's sparsetools complex_wrapper (and numpy): (ac - bd) + (ad + bc)i.
 template <typename T> __device__ __forceinline__ T mul_rn(T a, T b);
 template <> __device__ __forceinline__ double mul_rn<double>(double a, double b) { return __dmul_rn(a, b); }
 template <> __device__ __forceinline__ float mul_rn<float>(float a, float b) { return __fmul_rn(a, b); }
+template <> __device__ __forceinline__ cplx<double> mul_rn<cplx<double>>(cplx<double> a, cplx<double> b) {
+    return cplx<double>(__dsub_rn(__dmul_rn(a.re, b.re), __dmul_rn(a.im, b.im)),
+                        __dadd_rn(__dmul_rn(a.re, b.im), __dmul_rn(a.im, b.re)));
+}
+template <> __device__ __forceinline__ cplx<float> mul_rn<cplx<float>>(cplx<float> a, cplx<float> b) {
+    return cplx<float>(__fsub_rn(__fmul_rn(a.re, b.re), __fmul_rn(a.im, b.im)),
+                       __fadd_rn(__fmul_rn(a.re, b.im), __fmul_rn(a.im, b.re)));
+}
 template <typename T> __device__ __forceinline__ T add_rn(T a, T b);
 template <> __device__ __forceinline__ double add_rn<double>(double a, double b) { return __dadd_rn(a, b); }
 template <> __device__ __forceinline__ float add_rn<float>(float a, float b) { return __fadd_rn(a, b); }
+template <> __device__ __forceinline__ cplx<double> add_rn<cplx<double>>(cplx<double> a, cplx<double> b) {
+    return cplx<double>(__dadd_rn(a.re, b.re), __dadd_rn(a.im, b.im));
+}
+template <> __device__ __forceinline__ cplx<float> add_rn<cplx<float>>(cplx<float> a, cplx<float> b) {
+    return cplx<float>(__fadd_rn(a.re, b.re), __fadd_rn(a.im, b.im));
+}
+
+// Lane shuffle of a value of any of the four value types.
+template <typename T> __device__ __forceinline__ T shfl_v(T v, int s) { return __shfl(v, s, WAVE); }
+template <typename R> __device__ __forceinline__ cplx<R> shfl_v(cplx<R> v, int s) {
+    return cplx<R>(__shfl(v.re, s, WAVE), __shfl(v.im, s, WAVE));
+}
 
 // LDS footprint per wave.
 template <typename T> struct NumGeom {

@@ -91,7 +91,26 @@ namespace {
 
 inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 
-inline size_t vbytes(spg_dtype_t t) { return t == SPG_R_64F ? 8 : 4; }
+inline size_t vbytes(spg_dtype_t t) {
+    return t == SPG_C_64F ? 16 : (t == SPG_R_64F || t == SPG_C_32F) ? 8 : 4;
+}
+
+// bytes of one packed B record (BRec<T>) of the tile path
+inline size_t brec_bytes(spg_dtype_t t) {
+    return t == SPG_C_64F ? 24 : (t == SPG_R_64F || t == SPG_C_32F) ? 16 : 8;
+}
+
+// Runs f(T{}) with T the C++ type of value type t.
+template <typename F>
+spg_status_t dispatch_value(spg_dtype_t t, F&& f) {
+    switch (t) {
+        case SPG_R_32F: return f(float(0));
+        case SPG_R_64F: return f(double(0));
+        case SPG_C_32F: return f(cplx<float>(0));
+        case SPG_C_64F: return f(cplx<double>(0));
+    }
+    return SPG_STATUS_NOT_SUPPORTED;
+}
 
 inline int64_t grid_for(int64_t rows, int per_block) { return (rows + per_block - 1) / per_block; }
 
@@ -191,7 +210,9 @@ spg_status_t check_csr(const spg_csr_t* M) {
     if (M->cols > 2147483647LL) return SPG_STATUS_NOT_SUPPORTED;   // int32 column indices
     if (M->indptr_type != SPG_INDEX_32I && M->indptr_type != SPG_INDEX_64I)
         return SPG_STATUS_INVALID_VALUE;
-    if (M->value_type != SPG_R_32F && M->value_type != SPG_R_64F) return SPG_STATUS_NOT_SUPPORTED;
+    if (M->value_type != SPG_R_32F && M->value_type != SPG_R_64F && M->value_type != SPG_C_32F &&
+        M->value_type != SPG_C_64F)
+        return SPG_STATUS_NOT_SUPPORTED;
     if (M->indptr_type == SPG_INDEX_32I && M->nnz > 2147483647LL) return SPG_STATUS_INVALID_VALUE;
     if (!M->indptr && M->rows >= 0) return SPG_STATUS_INVALID_VALUE;
     if (M->nnz > 0 && (!M->indices || !M->values)) return SPG_STATUS_INVALID_VALUE;
@@ -325,7 +346,7 @@ Layout make_layout(const spg_plan_s& p) {
     L.spill = off;   off = align_up(off + sizeof(int32_t) * 2 * (size_t)std::max<int64_t>(p.A.rows, 1));
     if (p.use_tile) {
         L.tidx = off;  off = align_up(off + sizeof(uint2) * (size_t)p.B.rows * (size_t)p.G);
-        L.brec = off;  off = align_up(off + (p.A.value_type == SPG_R_64F ? 16 : 8) * (size_t)std::max<int64_t>(p.B.nnz, 1));
+        L.brec = off;  off = align_up(off + brec_bytes(p.A.value_type) * (size_t)std::max<int64_t>(p.B.nnz, 1));
         L.items = off; off = align_up(off + sizeof(int64_t) * (size_t)(tile_items(p) + 1));
         L.bitmap = off; off = align_up(off + sizeof(uint32_t) * (size_t)tile_items(p) * (size_t)((1 << p.tws) >> 5));
     }
@@ -827,16 +848,16 @@ spg_status_t spg_symbolic(spg_handle_t h, spg_plan_t p, void* C_indptr, spg_inde
     SPG_HIP(h, hipSetDevice(h->device));
     spg_status_t st;
     const bool i64 = p->A.indptr_type == SPG_INDEX_64I;
-    const bool f64 = p->A.value_type == SPG_R_64F;
     if (fused_alg1(*p) && !p->fused_failed) {
         // ALG1 single pass: one launch writes C compact into tj/tx and its row pointer; a
         // repeated call (int64 retry) only rescans the row counts it recorded
         ++p->symbolic_runs;
         if (!p->counts_ready) {
-            st = f64 ? (i64 ? alg1_fused_typed<double, int64_t>(h, *p, C_indptr, C_indptr_type)
-                            : alg1_fused_typed<double, int32_t>(h, *p, C_indptr, C_indptr_type))
-                     : (i64 ? alg1_fused_typed<float, int64_t>(h, *p, C_indptr, C_indptr_type)
-                            : alg1_fused_typed<float, int32_t>(h, *p, C_indptr, C_indptr_type));
+            st = dispatch_value(p->A.value_type, [&](auto tag) {
+                using T = decltype(tag);
+                return i64 ? alg1_fused_typed<T, int64_t>(h, *p, C_indptr, C_indptr_type)
+                           : alg1_fused_typed<T, int32_t>(h, *p, C_indptr, C_indptr_type);
+            });
         } else {
             const int64_t tiles = scan_tiles(p->A.rows) + 1;
             SPG_HIP(h, hipMemsetAsync(p->scan_status + tiles, 0, sizeof(unsigned long long) * tiles, h->stream));
@@ -880,10 +901,10 @@ spg_status_t spg_symbolic(spg_handle_t h, spg_plan_t p, void* C_indptr, spg_inde
     }
     if (!p->counts_ready) {
         if (p->alg == SPG_ALG1 && !p->use_tile && !fused_alg1(*p)) {
-            if (f64)
-                st = i64 ? alg1_compute<double, int64_t>(h, *p) : alg1_compute<double, int32_t>(h, *p);
-            else
-                st = i64 ? alg1_compute<float, int64_t>(h, *p) : alg1_compute<float, int32_t>(h, *p);
+            st = dispatch_value(p->A.value_type, [&](auto tag) {
+                using T = decltype(tag);
+                return i64 ? alg1_compute<T, int64_t>(h, *p) : alg1_compute<T, int32_t>(h, *p);
+            });
         } else {
             st = i64 ? symbolic_typed<int64_t>(h, *p) : symbolic_typed<int32_t>(h, *p);
         }
@@ -920,18 +941,15 @@ spg_status_t spg_numeric(spg_handle_t h, spg_plan_t p, const void* alpha, spg_cs
     SPG_HIP(h, hipSetDevice(h->device));
     const bool i64 = p->A.indptr_type == SPG_INDEX_64I;
     const bool c64 = C->indptr_type == SPG_INDEX_64I;
-    if (p->A.value_type == SPG_R_64F) {
-        const double a = *(const double*)alpha;
-        if (i64) return c64 ? numeric_typed<double, int64_t, int64_t>(h, *p, *C, a)
-                            : numeric_typed<double, int64_t, int32_t>(h, *p, *C, a);
-        return c64 ? numeric_typed<double, int32_t, int64_t>(h, *p, *C, a)
-                   : numeric_typed<double, int32_t, int32_t>(h, *p, *C, a);
-    }
-    const float a = *(const float*)alpha;
-    if (i64) return c64 ? numeric_typed<float, int64_t, int64_t>(h, *p, *C, a)
-                        : numeric_typed<float, int64_t, int32_t>(h, *p, *C, a);
-    return c64 ? numeric_typed<float, int32_t, int64_t>(h, *p, *C, a)
-               : numeric_typed<float, int32_t, int32_t>(h, *p, *C, a);
+    return dispatch_value(p->A.value_type, [&](auto tag) {
+        using T = decltype(tag);
+        T a;
+        std::memcpy(&a, alpha, sizeof(T));   // host value of C's type (a (re, im) pair if complex)
+        if (i64) return c64 ? numeric_typed<T, int64_t, int64_t>(h, *p, *C, a)
+                            : numeric_typed<T, int64_t, int32_t>(h, *p, *C, a);
+        return c64 ? numeric_typed<T, int32_t, int64_t>(h, *p, *C, a)
+                   : numeric_typed<T, int32_t, int32_t>(h, *p, *C, a);
+    });
 }
 
 spg_status_t spg_result_in_workspace(spg_plan_t p, void** indices, void** values) {

@@ -247,7 +247,7 @@ __global__ __launch_bounds__(BLOCK) void k_numeric(
                     }
                 }
                 for_each_product(beg, cnt, marker, [&](bool v, int s, long long idx) {
-                    const T as = __shfl(av, s, WAVE);
+                    const T as = shfl_v(av, s);
                     int col = 0;
                     T bv = (T)0;
                     if (v) {
@@ -412,7 +412,7 @@ __device__ __forceinline__ int chunk_src(L& S, int l, int cnt, int off, int c0, 
 }
 
 template <typename T, typename IP, typename OFF, int MODE, typename G>
-__global__ __launch_bounds__(G::WPB * WAVE, 5) void k_short(
+__global__ __launch_bounds__(G::WPB * WAVE, sizeof(T) <= 8 ? 5 : 2) void k_short(
     int64_t row0, int64_t nrows, int64_t ncols, const IP* __restrict__ Ap,
     const int32_t* __restrict__ Aj, const T* __restrict__ Ax, const IP* __restrict__ Bp,
     const int32_t* __restrict__ Bj, const T* __restrict__ Bx, const OFF* __restrict__ Coff,

@@ -79,14 +79,17 @@ __global__ __launch_bounds__(256) void k_tile_index(int64_t rows, const IP* __re
 }
 
 // B packed as (column, value) records for the numeric tile pass: one load brings both.
-template <typename T> struct BRec;
+template <typename T> struct BRec { int32_t c; int32_t pad; T v; };   // complex: 16 / 24 B
 template <> struct __attribute__((aligned(16))) BRec<double> { int32_t c; int32_t pad; double v; };
 template <> struct __attribute__((aligned(8))) BRec<float> { int32_t c; float v; };
 
 // One load per record: 16 bytes (f64) or 8 bytes (f32).
 template <typename T, typename IP>
 __device__ __forceinline__ void load_rec(const BRec<T>* __restrict__ rec, IP i, int& c, T& v) {
-    if constexpr (sizeof(T) == 8) {
+    if constexpr (!std::is_same<T, double>::value && !std::is_same<T, float>::value) {
+        c = rec[i].c;
+        v = rec[i].v;
+    } else if constexpr (sizeof(T) == 8) {
         const uint4 q = reinterpret_cast<const uint4*>(rec)[i];
         c = (int)q.x;
         v = __hiloint2double((int)q.w, (int)q.z);
@@ -103,7 +106,7 @@ __global__ __launch_bounds__(256) void k_pack_b(int64_t nnz, const int32_t* __re
     for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < nnz; e += (int64_t)gridDim.x * 256) {
         BRec<T> r;
         r.c = Bj[e];
-        if constexpr (sizeof(BRec<T>) == 16) r.pad = 0;
+        if constexpr (!std::is_same<T, float>::value) r.pad = 0;
         r.v = Bx[e];
         rec[e] = r;
     }
@@ -278,7 +281,7 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile(
     const BRec<T>* __restrict__ brec, const uint2* __restrict__ tidx,
     const uint32_t* __restrict__ bitmap, const int64_t* __restrict__ item_off,
     int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha) {
-    constexpr int U = 8;
+    constexpr int U = sizeof(T) > 8 ? 4 : 8;   // chunks in flight (complex128: half)
     __shared__ __attribute__((aligned(16))) NumLds<T, IP> lds[TILE_WPB];
     const int l = lane_id();
     const int wv = uniform((int)(threadIdx.x >> 6));
@@ -325,7 +328,7 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile(
         // The first NB batches of A entries (rows of <= NB*64 entries: all of them): every
         // lane's A entry, value, tile segment and B row start, loaded at once up front (two
         // dependent load levels per item instead of two per batch).
-        constexpr int NB = 8;
+        constexpr int NB = sizeof(T) > 8 ? 4 : 8;
         int32_t kq[NB];
         T aq[NB];
         uint2 sq[NB];

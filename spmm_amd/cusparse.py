@@ -29,7 +29,11 @@ from . import _lib
 from ._lib import SpgCsr, SpgError, check
 from .sparse import csr_matrix
 
-_VT = {torch.float32: _lib.SPG_R_32F, torch.float64: _lib.SPG_R_64F}
+_VT = {torch.float32: _lib.SPG_R_32F, torch.float64: _lib.SPG_R_64F,
+       torch.complex64: _lib.SPG_C_32F, torch.complex128: _lib.SPG_C_64F}
+# host alpha of C's value type: one scalar, or a (real, imag) pair for complex
+_ALPHA_CT = {torch.float32: (ctypes.c_float, 1), torch.float64: (ctypes.c_double, 1),
+             torch.complex64: (ctypes.c_float, 2), torch.complex128: (ctypes.c_double, 2)}
 _IT = {torch.int32: _lib.SPG_INDEX_32I, torch.int64: _lib.SPG_INDEX_64I}
 _ALG = {1: _lib.SPG_ALG1, 2: _lib.SPG_ALG2, 3: _lib.SPG_ALG3}
 
@@ -92,8 +96,8 @@ def validate_csr(m: csr_matrix) -> int:
 
 def _cast_common_type(a: csr_matrix, b: csr_matrix):
     dt = np.promote_types(a.dtype, b.dtype)
-    if dt not in (np.float32, np.float64):
-        raise TypeError(f"spgemm supports float32/float64, got {dt}")
+    if dt not in (np.float32, np.float64, np.complex64, np.complex128):
+        raise TypeError(f"spgemm supports float32/float64/complex64/complex128, got {dt}")
     return a.astype(dt), b.astype(dt)
 
 
@@ -178,8 +182,8 @@ def spgemm(a, b, alpha=1, alg=0, chunk_fraction=0.2, verbose=False):
         c = csr_matrix._from_parts(data, indices, indptr, (m, n), canonical=True)
         vc = SpgCsr(m, n, nnzc, indptr.data_ptr(), indices.data_ptr() if nnzc else 0,
                     data.data_ptr() if nnzc else 0, _IT[indptr.dtype], _VT[data.dtype])
-        ctype = ctypes.c_double if a.data.dtype == torch.float64 else ctypes.c_float
-        al = ctype(float(alpha))
+        ct, nparts = _ALPHA_CT[a.data.dtype]
+        al = (ct * 2)(complex(alpha).real, complex(alpha).imag) if nparts == 2 else ct(float(alpha))
         check(lib.spg_numeric(h.ptr, plan, ctypes.byref(al), ctypes.byref(vc)), "spg_numeric")
         peak = ctypes.c_size_t(0)
         lib.spg_peak_bytes(plan, ctypes.byref(peak))

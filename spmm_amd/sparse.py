@@ -21,6 +21,7 @@ import numpy as np
 import torch
 
 _TORCH_OF = {np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64,
+             np.dtype(np.complex64): torch.complex64, np.dtype(np.complex128): torch.complex128,
              np.dtype(np.int32): torch.int32, np.dtype(np.int64): torch.int64}
 _NP_OF = {v: k for k, v in _TORCH_OF.items()}
 
@@ -118,7 +119,7 @@ class csr_matrix(_SparseBase):
             self._canonical = canon
         else:
             raise TypeError(f"unsupported csr_matrix argument {type(arg1)}")
-        if self.data.dtype not in (torch.float32, torch.float64):
+        if self.data.dtype not in (torch.float32, torch.float64, torch.complex64, torch.complex128):
             raise TypeError(f"unsupported dtype {self.data.dtype}")
         if self.indptr.numel() != self._shape[0] + 1:
             raise ValueError("indptr length must be rows + 1")

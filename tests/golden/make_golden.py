@@ -141,6 +141,25 @@ def main():
     B = rand(32, 48, 0.2, np.random.default_rng(1), np.float64)
     cases.append(save("emptyA_64x32x48_f64", A, B, note="A has no entries"))
 
+    # complex values (upstream TestSpgemm dtypes complex64/complex128, test_cusparse.py:
+    # 372-375): the shapes with alpha 0.5, and larger random products with complex normal
+    # values (scipy's complex_wrapper arithmetic: (ac - bd) + (ad + bc)i, no FMA)
+    for dt in (np.complex64, np.complex128):
+        tag = "c64" if dt == np.complex64 else "c128"
+        for (m, n, k) in [(2, 3, 4), (4, 3, 2)]:
+            rng = np.random.default_rng(2000 + m)
+            a = rand(m, k, 0.5, rng, dt)
+            b = rand(k, n, 0.5, rng, dt)
+            a.data = a.data + 1j * rng.uniform(size=a.nnz)
+            b.data = b.data + 1j * rng.uniform(size=b.nnz)
+            cases.append(save(f"testspgemm_{m}x{n}x{k}_{tag}", a, b, alpha=0.5,
+                              note="upstream TestSpgemm complex, alpha=0.5"))
+        rng = np.random.default_rng(31 if dt == np.complex64 else 32)
+        cn = lambda s: rng.standard_normal(s) + 1j * rng.standard_normal(s)
+        A = rand(400, 300, 0.03, rng, dt, cn)
+        B = rand(300, 500, 0.03, rng, dt, cn)
+        cases.append(save(f"normal_400x300x500_{tag}", A, B, alpha=-0.75, note="complex normal, alpha"))
+
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump({"generator": "tests/golden/make_golden.py",
                    "truth": f"scipy {scipy.__version__} csr@csr, numpy {np.__version__}",

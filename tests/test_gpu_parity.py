@@ -397,3 +397,49 @@ def test_alg1_single_pass_estimate_overflow():
     ref = oracle.spgemm(A, B, alpha=1.5, keep_zeros=True, sort=True)
     assert len(ref[1]) > 10 * A.nnz * (B.nnz / B.shape[0])
     _assert_same(_gpu(A, B, alg=1, alpha=1.5), ref)
+
+
+def _cplx_random(m, n, density, rng, dt):
+    M = sp.random(m, n, density=density, format="csr", random_state=rng, dtype=np.float64)
+    M = sp.csr_matrix((M.data + 1j * rng.standard_normal(M.nnz), M.indices, M.indptr),
+                      shape=M.shape).astype(dt)
+    M.sort_indices()
+    return M
+
+
+@pytest.mark.parametrize("dt", [np.complex64, np.complex128])
+@pytest.mark.parametrize("m,k,n,density", [
+    (2048, 2048, 2048, 0.004),      # short-row kernel
+    (600, 3000, 4000, 0.03),        # tile path (dense C rows)
+    (300, 2000, 200000, 2e-4),      # general windowed kernel (very wide, sparse C)
+])
+@pytest.mark.parametrize("alg", [1, 2, 3])
+def test_complex_bitexact(dt, m, k, n, density, alg):
+    """complex64 / complex128 (the reference's TestSpgemm dtypes): scipy's complex product
+    (ac - bd) + (ad + bc)i, summed in A's entry order, alpha complex."""
+    rng = np.random.default_rng(m + n + (7 if dt == np.complex64 else 9))
+    A = _cplx_random(m, k, density, rng, dt)
+    B = _cplx_random(k, n, density, rng, dt)
+    alpha = 0.5 - 0.25j
+    _assert_same(_gpu(A, B, alg=alg, alpha=alpha), oracle.spgemm(A, B, alpha=alpha, keep_zeros=True, sort=True))
+
+
+def test_upstream_testspgemm_complex():
+    """test_cusparse.py:372-411 with dtype complex64 / complex128 (alpha 0.5), including
+    the (100000, 100000, 50) run-only case."""
+    from spmm_amd import cusparse
+    from spmm_amd.sparse import csr_matrix
+    for dt in (np.complex64, np.complex128):
+        for (m, n, k) in [(2, 3, 4), (4, 3, 2), (100000, 100000, 50)]:
+            rng = np.random.default_rng(m + n + k + 5)
+            a = sp.random(m, k, density=0.5, dtype=dt, random_state=rng, format="csr")
+            b = sp.random(k, n, density=0.5, dtype=dt, random_state=rng, format="csr")
+            a.data = (a.data + 1j * rng.uniform(size=a.nnz)).astype(dt)
+            b.data = (b.data + 1j * rng.uniform(size=b.nnz)).astype(dt)
+            a.sort_indices(); b.sort_indices()
+            c = cusparse.spgemm(csr_matrix(a, device=_dev()), csr_matrix(b, device=_dev()), alpha=0.5)
+            assert c.dtype == dt
+            if m == 100000:
+                assert c.nnz > 0
+                continue
+            np.testing.assert_array_almost_equal(c.toarray(), (0.5 * a.dot(b)).toarray())
