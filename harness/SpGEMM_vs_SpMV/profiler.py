@@ -1,14 +1,16 @@
 #!/usr/bin/env python3
-"""scipy CPU SpGEMM vs spmm_amd GPU SpGEMM, end to end (port of the SpGEMM part of
+"""scipy CPU SpGEMM and SpMV vs spmm_amd GPU SpGEMM and SpMV, end to end (port of
 SpGEMM_vs_SpMV/profiler.py :380-528; the figure SPGEMM-gpu-speedup.png).
 
 CPU: scipy ``A @ B`` for CSR/CSC/COO operand combinations, each run in a forked child
 (time + ΔRSS, profiler.py:116-178), median of --runs.  GPU: the same products with the host
 matrices converted and uploaded inside the timed region (H2D included, as the reference
 times ``to_gpu_sparse`` + ``@`` together, profiler.py:485-498); CSC/COO operands go through
-CSR conversion on the device.  The SpMV half of the reference script is a different kernel
-and out of scope here.  Deliberate fix: B uses seed+1 (the reference reuses the seed, so
-A == B, profiler.py:397-398).
+CSR conversion on the device.  SpMV rows (profiler.py:410-411, 500-501): ``A @ C`` with C a
+dense vector of n entries (seed+2), A in each format, on the CPU (scipy) and the GPU
+(spmm_amd.cusparse.spmv through ``__matmul__``, x uploaded inside the timed region as the
+reference's ``cp.asarray(C)``).  Deliberate fix: B uses seed+1 (the reference reuses the
+seed, so A == B, profiler.py:397-398).
 """
 import argparse
 import os
@@ -56,6 +58,7 @@ def main():
     dtype = np.float32 if args.dtype == "float32" else np.float64
     A = {f: make(args.m, args.n, args.densityA, f, dtype, args.seed) for f in args.formats}
     B = {f: make(args.n, args.p, args.densityB, f, dtype, args.seed + 1) for f in args.formats}
+    C = np.random.default_rng(args.seed + 2).standard_normal(args.n).astype(dtype)
     ctx = threadpool_limits(limits=args.threads) if threadpool_limits and args.threads > 0 else None
 
     cpu = []
@@ -64,6 +67,8 @@ def main():
     for fa in args.formats:
         for fb in args.formats:
             cpu.append(repeat_cpu(f"A_{fa} @ B_{fb} (SpGEMM)", lambda a=A[fa], b=B[fb]: a @ b, args.runs))
+    for fa in args.formats:
+        cpu.append(repeat_cpu(f"A_{fa} @ C (SpMV, dense vec)", lambda a=A[fa]: a @ C, args.runs))
     if ctx:
         ctx.__exit__(None, None, None)
     print("\n=== Results (CPU/SciPy) ===")
@@ -87,6 +92,9 @@ def main():
         for fb in args.formats:
             fn = (lambda a=A[fa], b=B[fb], fa=fa, fb=fb: TO_GPU[fa](a) @ TO_GPU[fb](b))
             gpu.append(repeat_gpu(f"A_{fa} @ B_{fb} (SpGEMM)", fn, args.runs))
+    for fa in args.formats:
+        fn = (lambda a=A[fa], fa=fa: TO_GPU[fa](a) @ torch.from_numpy(C).cuda())
+        gpu.append(repeat_gpu(f"A_{fa} @ C (SpMV, dense vec)", fn, args.runs))
     print("\n=== Results ===")
     header = f"{'name':36}  {'time(ms)':>10}  {'ΔPeak VRAM':>12}  {'out_shape':>16}  {'speedup':>8}"
     print(header)

@@ -162,6 +162,15 @@ spg_status_t spg_symbolic(spg_handle_t handle, spg_plan_t plan, void *C_indptr,
 spg_status_t spg_numeric(spg_handle_t handle, spg_plan_t plan, const void *alpha,
                          spg_csr_t *C);
 
+/* Sparse matrix x dense vector: y = alpha * A x + beta * y (A CSR, x of A.cols entries,
+ * y of A.rows entries, all of A's value type; alpha/beta host values).  Each row is summed
+ * in A's entry order from 0, so the result equals scipy's csr_matvec bit for bit (beta = 0,
+ * alpha = 1).  Stream-ordered; does not wait.  (cusparseSpMV as called by
+ * cupyx.cusparse.spmv, modify_src/cupy-src/cupyx/cusparse.py:1373-1432; the SpMV half of
+ * SpGEMM_vs_SpMV/profiler.py:410-411.) */
+spg_status_t spg_spmv(spg_handle_t handle, const spg_csr_t *A, const void *x, const void *alpha,
+                      const void *beta, void *y);
+
 /* ALG1 single pass: after spg_symbolic, C's column indices and values may already sit
  * compact in the workspace (nnzC entries at *indices / *values; NULL otherwise).  A
  * caller may hand exactly these pointers to spg_numeric as C->indices / C->values: the
@@ -203,6 +212,7 @@ typedef enum {
     SPG_PHASE_VALIDATE = 5,   /* k_validate                                         */
     SPG_PHASE_SPILL = 6,      /* k_symbolic / k_numeric over the rows the short-row */
                               /* kernel handed on (list mode); k_tile_index         */
+    SPG_PHASE_SPMV = 7,       /* k_spmv                                             */
     SPG_NUM_PHASES = 8
 } spg_phase_t;
 

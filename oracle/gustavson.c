@@ -242,3 +242,23 @@ int orc_has_canonical_format(int64_t n_row, const int64_t *Ap, const int32_t *Aj
     }
     return 1;
 }
+
+/* CSR x dense vector (scipy `csr_matvec`, reached from csr_matrix @ ndarray -> _mul_vector,
+ * the SpMV half of SpGEMM_vs_SpMV/profiler.py:410-411): y[i] = ((0 + a_i0 x_j0) + a_i1 x_j1)
+ * + ..., every product and sum rounded on its own, A's entries in stored order; then
+ * y = alpha * y when alpha != 1 (numpy's scalar multiply). */
+#define DEFINE_SPMV(T, SUF)                                                                 \
+    void orc_spmv_##SUF(int64_t n_row, const int64_t *Ap, const int32_t *Aj, const T *Ax,   \
+                        const T *x, T alpha, T *y)                                          \
+    {                                                                                       \
+        for (int64_t i = 0; i < n_row; ++i) {                                               \
+            T sum = zero_##SUF();                                                           \
+            for (int64_t jj = Ap[i]; jj < Ap[i + 1]; ++jj)                                  \
+                sum = add_##SUF(sum, mul_##SUF(Ax[jj], x[Aj[jj]]));                         \
+            y[i] = one_##SUF(alpha) ? sum : mul_##SUF(alpha, sum);                          \
+        }                                                                                   \
+    }
+DEFINE_SPMV(double, f64)
+DEFINE_SPMV(float, f32)
+DEFINE_SPMV(orc_c64, c64)
+DEFINE_SPMV(orc_c128, c128)

@@ -43,9 +43,9 @@ STATUS_OVERFLOW = 100
 EXPORTS = ("spg_version", "spg_status_string", "spg_create", "spg_destroy", "spg_set_stream",
            "spg_last_hip_error", "spg_plan", "spg_num_products", "spg_symbolic",
            "spg_numeric", "spg_peak_bytes", "spg_validate_csr", "spg_plan_destroy",
-           "spg_set_timing", "spg_get_timing", "spg_result_in_workspace")
+           "spg_set_timing", "spg_get_timing", "spg_result_in_workspace", "spg_spmv")
 
-PHASES = ("products", "scan", "symbolic", "numeric", "compact", "validate", "spill")
+PHASES = ("products", "scan", "symbolic", "numeric", "compact", "validate", "spill", "spmv")
 NUM_PHASES = 8
 
 
@@ -101,6 +101,7 @@ def load():
                                         ctypes.POINTER(sz), vp, ctypes.POINTER(vp)]),
             "spg_num_products": (ctypes.c_int, [vp, vp, ctypes.POINTER(i64)]),
             "spg_result_in_workspace": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp)]),
+            "spg_spmv": (ctypes.c_int, [vp, csrp, vp, vp, vp, vp]),
             "spg_symbolic": (ctypes.c_int, [vp, vp, vp, ctypes.c_int, ctypes.POINTER(i64)]),
             "spg_numeric": (ctypes.c_int, [vp, vp, vp, csrp]),
             "spg_peak_bytes": (ctypes.c_int, [vp, ctypes.POINTER(sz)]),

@@ -15,6 +15,7 @@
 #include "spgemm.h"
 #include "spgemm_kernels.hpp"
 #include "spgemm_tile.hpp"
+#include "spgemm_spmv.hpp"
 
 using namespace spg;
 
@@ -949,6 +950,36 @@ spg_status_t spg_numeric(spg_handle_t h, spg_plan_t p, const void* alpha, spg_cs
                             : numeric_typed<T, int64_t, int32_t>(h, *p, *C, a);
         return c64 ? numeric_typed<T, int32_t, int64_t>(h, *p, *C, a)
                    : numeric_typed<T, int32_t, int32_t>(h, *p, *C, a);
+    });
+}
+
+spg_status_t spg_spmv(spg_handle_t h, const spg_csr_t* A, const void* x, const void* alpha,
+                      const void* beta, void* y) {
+    if (!h) return SPG_STATUS_NOT_INITIALIZED;
+    spg_status_t st = check_csr(A);
+    if (st) return st;
+    if (!alpha || !beta || (A->rows > 0 && !y) || (A->cols > 0 && A->nnz > 0 && !x))
+        return SPG_STATUS_INVALID_VALUE;
+    if (A->rows == 0) return SPG_STATUS_SUCCESS;
+    SPG_HIP(h, hipSetDevice(h->device));
+    const bool i64 = A->indptr_type == SPG_INDEX_64I;
+    return dispatch_value(A->value_type, [&](auto tag) {
+        using T = decltype(tag);
+        T al, be;
+        std::memcpy(&al, alpha, sizeof(T));
+        std::memcpy(&be, beta, sizeof(T));
+        const unsigned grid = (unsigned)grid_for(A->rows, SPMV_WPB * WAVE);
+        PhaseTimer pt(h, SPG_PHASE_SPMV);
+        if (i64)
+            hipLaunchKernelGGL((k_spmv<T, int64_t>), dim3(grid), dim3(SPMV_WPB * WAVE), 0, h->stream, A->rows,
+                               (const int64_t*)A->indptr, (const int32_t*)A->indices, (const T*)A->values,
+                               (const T*)x, al, be, (T*)y);
+        else
+            hipLaunchKernelGGL((k_spmv<T, int32_t>), dim3(grid), dim3(SPMV_WPB * WAVE), 0, h->stream, A->rows,
+                               (const int32_t*)A->indptr, (const int32_t*)A->indices, (const T*)A->values,
+                               (const T*)x, al, be, (T*)y);
+        SPG_LAUNCHED(h);
+        return SPG_STATUS_SUCCESS;
     });
 }
 

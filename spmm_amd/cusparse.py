@@ -58,7 +58,7 @@ def check_availability(name: str) -> bool:
     """True when the named routine can run here (a gfx950 device and the built library).
     Memoized like the reference's ``@_util.memoize()`` check (cusparse.py:169-186)."""
     global _available
-    if name not in ("spgemm", "validate_csr"):
+    if name not in ("spgemm", "spmv", "validate_csr"):
         raise ValueError(f"No available version information specified for {name}")
     if _available is None:
         try:
@@ -198,6 +198,61 @@ def spgemm(a, b, alpha=1, alg=0, chunk_fraction=0.2, verbose=False):
         lib.spg_plan_destroy(plan)
 
 
+def spmv(a, x, y=None, alpha=1, beta=0, transa=False):
+    """y = alpha * op(A) x + beta * y -- the drop-in for ``cupyx.cusparse.spmv``
+    (modify_src/cupy-src/cupyx/cusparse.py:1373-1432), on ``spg_spmv``.
+
+    A is csr_matrix, csc_matrix or coo_matrix (CSC goes through its transpose as the
+    reference does, COO through CSR).  x, y are 1-D tensors (or numpy arrays, uploaded).
+    With CSR A, alpha = 1 and beta = 0 the result equals scipy's ``A @ x`` bit for bit.
+    """
+    from .sparse import coo_matrix, csc_matrix
+    if not check_availability("spmv"):
+        raise RuntimeError("spmv is not available.")
+    if isinstance(a, csc_matrix):
+        a = a.T
+        transa = not transa
+    if not isinstance(a, (csr_matrix, coo_matrix)):
+        raise TypeError("unsupported type (actual: {})".format(type(a)))
+    if isinstance(a, coo_matrix):
+        a = a.tocsr()
+    if transa:
+        a = a.transpose_csr()
+    dev = a.device
+    if not isinstance(x, torch.Tensor):
+        x = torch.from_numpy(np.ascontiguousarray(x))
+    x = x.to(dev)
+    if a.shape[1] != x.numel():
+        raise ValueError("dimension mismatch")
+    assert a.has_canonical_format
+    m = a.shape[0]
+    dt = np.promote_types(a.dtype, np.dtype(str(x.dtype).replace("torch.", "")))
+    if dt not in (np.float32, np.float64, np.complex64, np.complex128):
+        raise TypeError(f"spmv supports float32/float64/complex64/complex128, got {dt}")
+    a = a.astype(dt)
+    tdt = a.data.dtype
+    x = x.to(tdt).contiguous()
+    if y is None:
+        y = torch.zeros(m, dtype=tdt, device=dev)
+    else:
+        if not isinstance(y, torch.Tensor) or y.numel() != m:
+            raise ValueError("dimension mismatch")
+        if y.dtype != tdt or not y.is_contiguous():
+            raise TypeError("y must be a contiguous tensor of the result type")
+    if a.nnz == 0:       # the reference fills 0 (cusparse.py:1414-1416)
+        y.fill_(0)
+        return y
+    h = _handle_for(a)
+    va = _csr_view(a)
+    ct, nparts = _ALPHA_CT[tdt]
+    def host(v):
+        return (ct * 2)(complex(v).real, complex(v).imag) if nparts == 2 else ct(float(v))
+    al, be = host(alpha), host(beta)
+    check(h.lib.spg_spmv(h.ptr, ctypes.byref(va), ctypes.c_void_p(x.data_ptr()), ctypes.byref(al),
+                         ctypes.byref(be), ctypes.c_void_p(y.data_ptr())), "spg_spmv")
+    return y
+
+
 def num_products(a: csr_matrix, b: csr_matrix) -> int:
     """P = number of scalar products of A.B (cusparseSpGEMM_getNumProducts); GFLOPS = 2P/t."""
     h = _handle_for(a)
@@ -218,5 +273,5 @@ def num_products(a: csr_matrix, b: csr_matrix) -> int:
         h.lib.spg_plan_destroy(plan)
 
 
-__all__ = ["spgemm", "check_availability", "num_products", "validate_csr", "SpgError",
+__all__ = ["spgemm", "spmv", "check_availability", "num_products", "validate_csr", "SpgError",
            "last_stats"]

@@ -213,7 +213,8 @@ class csr_matrix(_SparseBase):
 
     # ------------------------------------------------------------------ products
     def __mul__(self, other):
-        """CSR x sparse: CuPy's _csr.py:151-166 order -- canonicalise both, then spgemm."""
+        """CSR x sparse: CuPy's _csr.py:151-166 order -- canonicalise both, then spgemm.
+        CSR x dense vector (_csr.py:190-216): canonicalise, then spmv."""
         from . import cusparse
         if isinstance(other, (csc_matrix, coo_matrix)):
             other = other.tocsr()
@@ -221,7 +222,18 @@ class csr_matrix(_SparseBase):
             self.sum_duplicates()
             other.sum_duplicates()
             return cusparse.spgemm(self, other)
+        if _is_vector(other):
+            self.sum_duplicates()
+            return cusparse.spmv(self, other)
         return NotImplemented
+
+    def transpose_csr(self) -> "csr_matrix":
+        """A^T as a canonical CSR matrix (through COO with rows and columns swapped)."""
+        m, n = self._shape
+        counts = (self.indptr[1:] - self.indptr[:-1]).to(torch.int64)
+        rows = torch.repeat_interleave(torch.arange(m, device=self.device), counts)
+        return coo_matrix((self.data, (self.indices.to(torch.int64), rows)), shape=(n, m),
+                          device=self.device).tocsr()
 
     def __matmul__(self, other):
         return self.__mul__(other)
@@ -234,9 +246,20 @@ class csr_matrix(_SparseBase):
                 f"{self.nnz} stored elements on {self.device}>")
 
 
+def _is_vector(x) -> bool:
+    return (isinstance(x, torch.Tensor) or isinstance(x, np.ndarray)) and x.ndim == 1
+
+
 class coo_matrix(_SparseBase):
     """Coordinate-format operand (only what CSR conversion needs)."""
     format = "coo"
+
+    def __matmul__(self, other):
+        """COO x dense vector -> spmv (through CSR)."""
+        if _is_vector(other):
+            from . import cusparse
+            return cusparse.spmv(self, other)
+        return super().__matmul__(other)
 
     def __init__(self, arg1, shape=None, device=None):
         if hasattr(arg1, "tocoo"):
@@ -276,6 +299,13 @@ class coo_matrix(_SparseBase):
 class csc_matrix(_SparseBase):
     """Compressed-column operand (only what CSR conversion needs)."""
     format = "csc"
+
+    def __matmul__(self, other):
+        """CSC x dense vector -> spmv (cusparse.py:1395-1401: csc.T is CSR, transposed op)."""
+        if _is_vector(other):
+            from . import cusparse
+            return cusparse.spmv(self, other)
+        return super().__matmul__(other)
 
     def __init__(self, arg1, device=None):
         S = arg1.tocsc()

@@ -13,6 +13,7 @@ output (its own linked-list column order, zeros dropped), plus ``alpha``.  The f
 inputs of the upstream CSR tests (test_csr.py:25-134) are reproduced as data.
 """
 import json
+import zlib
 import os
 
 import numpy as np
@@ -68,6 +69,40 @@ def rand(m, n, density, rng, dt, rvs=None):
                   data_rvs=rvs)
     M.sort_indices()
     return M
+
+
+def make_spmv():
+    """SpMV fixtures (csr_matrix @ dense vector, SpGEMM_vs_SpMV/profiler.py:410-411):
+    A, x, y = alpha * (A @ x) from scipy, one directory of their own."""
+    d = os.path.join(HERE, "spmv")
+    os.makedirs(d, exist_ok=True)
+    out = []
+    specs = [("n1024_d0.01_f64", 1024, 1024, 0.01, np.float64, 1.0),
+             ("rect_300x900_f32", 300, 900, 0.02, np.float32, -1.5),
+             ("n700_d0.03_c128", 700, 700, 0.03, np.complex128, 0.5),
+             ("rect_200x500_c64", 200, 500, 0.05, np.complex64, 1.0),
+             ("emptyrows_64x64_f64", 64, 64, 0.05, np.float64, 1.0)]
+    for name, m, n, dens, dt, alpha in specs:
+        rng = np.random.default_rng(zlib.crc32(name.encode()))
+        A = sp.random(m, n, density=dens, format="csr", random_state=rng, dtype=np.float64)
+        A.data = rng.standard_normal(A.nnz)
+        x = rng.standard_normal(n)
+        if np.dtype(dt).kind == "c":
+            A.data = A.data + 1j * rng.standard_normal(A.nnz)
+            x = x + 1j * rng.standard_normal(n)
+        if name.startswith("emptyrows"):
+            A = A.tolil(); A[::3, :] = 0; A = sp.csr_matrix(A); A.eliminate_zeros()
+        A = A.astype(dt); A.sort_indices()
+        x = x.astype(dt)
+        y = A @ x
+        if alpha != 1.0:
+            y = y * np.dtype(dt).type(alpha)
+        np.savez_compressed(os.path.join(d, name + ".npz"), A_shape=np.array(A.shape, np.int64),
+                            A_indptr=A.indptr.astype(np.int64), A_indices=A.indices.astype(np.int32),
+                            A_data=A.data, x=x, y=y, alpha=np.array(alpha, np.float64))
+        out.append({"name": name, "A": list(A.shape), "nnzA": int(A.nnz), "dtype": str(np.dtype(dt)),
+                    "alpha": alpha})
+    return out
 
 
 def main():
@@ -160,10 +195,12 @@ def main():
         B = rand(300, 500, 0.03, rng, dt, cn)
         cases.append(save(f"normal_400x300x500_{tag}", A, B, alpha=-0.75, note="complex normal, alpha"))
 
+    spmv_cases = make_spmv()
+
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump({"generator": "tests/golden/make_golden.py",
                    "truth": f"scipy {scipy.__version__} csr@csr, numpy {np.__version__}",
-                   "cases": cases}, f, indent=1)
+                   "cases": cases, "spmv_cases": spmv_cases}, f, indent=1)
     print(f"wrote {len(cases)} cases")
 
 

@@ -65,6 +65,15 @@ def test_alg_comparison_profiler():
         assert f"(alg={alg})" in r.stdout
 
 
+def test_spgemm_vs_spmv_profiler():
+    """SpGEMM_vs_SpMV/profiler.py port: CPU and GPU tables with SpGEMM and SpMV rows."""
+    r = run([sys.executable, os.path.join(H, "SpGEMM_vs_SpMV", "profiler.py"), "--m", "256",
+             "--n", "256", "--p", "256", "--densityA", "0.05", "--densityB", "0.05", "--runs", "3"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.stdout.count("(SpMV, dense vec)") == 6      # 3 formats, CPU and GPU tables
+    assert r.stdout.count("(SpGEMM)") == 18
+
+
 def test_dense_vs_sparse_harness():
     r = run([sys.executable, os.path.join(H, "dense_vs_sparseGEMM", "main.py"), "--size", "1024",
              "--density", "0.01", "--runs", "2", "--dtype", "float64"])

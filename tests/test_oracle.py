@@ -4,7 +4,7 @@ import pytest
 import scipy.sparse as sp
 
 from oracle import oracle
-from tests.golden_cases import case_names, load
+from tests.golden_cases import case_names, load, load_spmv, spmv_case_names
 
 CASES = case_names()
 
@@ -74,3 +74,12 @@ def test_openmp_variant_identical():
 def test_canonical_check(name):
     A, _, _, _ = load(name)
     assert oracle.has_canonical_format(A) == bool(A.has_canonical_format)
+
+
+@pytest.mark.parametrize("name", spmv_case_names())
+def test_oracle_spmv_matches_scipy_golden(name):
+    """The SpMV restatement (scipy csr_matvec order) equals scipy's committed output bit for bit."""
+    A, x, y, alpha = load_spmv(name)
+    got = oracle.spmv(A, x, alpha=alpha)
+    assert got.dtype == y.dtype
+    assert np.array_equal(got.view(np.uint8), y.view(np.uint8))
