@@ -8,7 +8,7 @@ ARCH     ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -Wall
 LIB      := spmm_amd/lib/libmi355_spgemm.so
 SRC      := spmm_amd/csrc/spgemm.hip
-HDRS     := include/spgemm.h spmm_amd/csrc/spg_device.hpp spmm_amd/csrc/spgemm_kernels.hpp
+HDRS     := include/spgemm.h $(wildcard spmm_amd/csrc/*.hpp)
 DRIVERS  := drivers/bin/spgemm_from_txt_alg1 drivers/bin/spgemm_from_txt_alg2 drivers/bin/spgemm_from_txt_alg3
 
 all: lib drivers oracle

@@ -8,6 +8,8 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -16,6 +18,7 @@
 #include "spgemm_kernels.hpp"
 #include "spgemm_tile.hpp"
 #include "spgemm_spmv.hpp"
+#include "spgemm_row.hpp"
 
 using namespace spg;
 
@@ -63,6 +66,7 @@ struct spg_plan_s {
     int32_t* spill = nullptr;       // rows the short-row kernel hands to the general kernel
     unsigned long long* scan_status = nullptr;   // look-back scan: ticket + one word per tile
     bool use_short = false;         // dispatch the short-row kernel first
+    bool use_row = true;            // short rows: k_row (false: the owner-round k_short)
     bool use_tile = false;          // wide-row path: (row, column tile) items
     int tws = 10;                   // log2 of the tile width
     int G = 1;                      // tiles per row
@@ -111,6 +115,25 @@ spg_status_t dispatch_value(spg_dtype_t t, F&& f) {
         case SPG_C_64F: return f(cplx<double>(0));
     }
     return SPG_STATUS_NOT_SUPPORTED;
+}
+
+// SPG_SHORT_KERNEL=short selects the owner-round k_short for short rows (A/B timing);
+// the default is k_row.  Read once per process.
+inline bool row_kernel_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("SPG_SHORT_KERNEL");
+        return !(e && std::strcmp(e, "short") == 0);
+    }();
+    return on;
+}
+
+// SPG_ALG1_ROW=1: the ALG1 single pass on k_row's arrival tree (experimental)
+inline bool row_lb_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("SPG_ALG1_ROW");
+        return e && std::strcmp(e, "1") == 0;
+    }();
+    return on;
 }
 
 inline int64_t grid_for(int64_t rows, int per_block) { return (rows + per_block - 1) / per_block; }
@@ -326,12 +349,41 @@ struct Layout {
 inline int64_t tile_items(const spg_plan_s& p) { return p.use_tile ? p.A.rows * p.G : 0; }
 
 // ALG1 runs as one fused pass (k_short SHORT_NUMLB) when the short-row kernel takes the shape
-inline bool fused_alg1(const spg_plan_s& p) { return p.alg == SPG_ALG1 && p.use_short && !p.use_tile; }
+inline bool fused_alg1(const spg_plan_s& p) {
+    return p.alg == SPG_ALG1 && p.use_short && !p.use_tile && p.A.rows <= (1LL << 24);
+}
+
+// ALG1 single pass on k_row: the 64-ary arrival tree over the rows (spgemm_row.hpp).
+// Words: agg[0] (rows) | agg[1] grp[1] | agg[2] grp[2] | agg[3] grp[3].
+inline size_t lbt_words(int64_t rows, LbTree* t = nullptr, unsigned long long* base = nullptr) {
+    long long n[4] = {rows, 0, 0, 0};
+    int top = 0;
+    while (top < 3 && n[top] > 64) {
+        n[top + 1] = (n[top] + 63) / 64;
+        ++top;
+    }
+    size_t w = (size_t)std::max<long long>(rows, 1);
+    if (t) {
+        t->agg[0] = base;
+        t->grp[0] = nullptr;
+        t->top = top;
+    }
+    for (int lv = 0; lv < 4; ++lv) {
+        if (t) t->n[lv] = n[lv];
+        if (lv == 0 || lv > top) continue;
+        if (t) {
+            t->agg[lv] = base + w;
+            t->grp[lv] = base + w + n[lv];
+        }
+        w += 2 * (size_t)n[lv];
+    }
+    return w;
+}
 
 // status words: products scan | row-pointer scan | item scan (tile path)
 inline size_t status_words(const spg_plan_s& p) {
     return 2 * (size_t)(scan_tiles(p.A.rows) + 1) + (p.use_tile ? (size_t)scan_tiles(tile_items(p)) + 1 : 0) +
-           (fused_alg1(p) ? (size_t)grid_for(p.A.rows, ShortSmall::WPB) + 1 : 0);
+           (fused_alg1(p) ? std::max(lbt_words(p.A.rows), (size_t)grid_for(p.A.rows, ShortSmall::WPB) + 1) : 0);
 }
 inline unsigned long long* item_scan_status(const spg_plan_s& p) {
     return p.scan_status + 2 * (scan_tiles(p.A.rows) + 1);
@@ -463,13 +515,21 @@ spg_status_t run_symbolic_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_
         int32_t* l1 = p.spill;
         {
             PhaseTimer pt(h, SPG_PHASE_SYMBOLIC);
-            hipLaunchKernelGGL((k_short<double, IP, int64_t, SHORT_SYM, ShortSmall>),
-                               dim3((unsigned)grid_for(n, ShortSmall::WPB)), dim3(ShortSmall::WPB * WAVE), 0,
-                               h->stream, r0, n, p.B.cols, Ap, Aj, (const double*)nullptr, Bp, Bj,
-                               (const double*)nullptr, (const int64_t*)nullptr, (int32_t*)nullptr,
-                               (double*)nullptr, 1.0, p.row_cnt, l1, cnt, (const int32_t*)nullptr,
-                               (const int32_t*)nullptr, (unsigned long long*)nullptr, (int64_t*)nullptr,
-                               (int64_t*)nullptr, (int64_t)0);
+            if (p.use_row)
+                hipLaunchKernelGGL((k_row<double, IP, int64_t, ROW_SYM, RowSmall>),
+                                   dim3((unsigned)grid_for(n, RowSmall::WPB)), dim3(RowSmall::WPB * WAVE), 0,
+                                   h->stream, r0, n, p.B.cols, Ap, Aj, (const double*)nullptr, Bp, Bj,
+                                   (const double*)nullptr, (const int64_t*)nullptr, (int32_t*)nullptr,
+                                   (double*)nullptr, 1.0, p.row_cnt, l1, cnt, LbTree{}, (int64_t*)nullptr,
+                                   (int64_t*)nullptr, (int64_t)0);
+            else
+                hipLaunchKernelGGL((k_short<double, IP, int64_t, SHORT_SYM, ShortSmall>),
+                                   dim3((unsigned)grid_for(n, ShortSmall::WPB)), dim3(ShortSmall::WPB * WAVE), 0,
+                                   h->stream, r0, n, p.B.cols, Ap, Aj, (const double*)nullptr, Bp, Bj,
+                                   (const double*)nullptr, (const int64_t*)nullptr, (int32_t*)nullptr,
+                                   (double*)nullptr, 1.0, p.row_cnt, l1, cnt, (const int32_t*)nullptr,
+                                   (const int32_t*)nullptr, (unsigned long long*)nullptr, (int64_t*)nullptr,
+                                   (int64_t*)nullptr, (int64_t)0);
             SPG_LAUNCHED(h);
         }
         PhaseTimer ps(h, SPG_PHASE_SPILL);
@@ -515,11 +575,17 @@ spg_status_t run_numeric_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_t
         int32_t* l1 = p.spill;
         {
             PhaseTimer pt(h, SPG_PHASE_NUMERIC);
-            hipLaunchKernelGGL((k_short<T, IP, OFF, MODE, ShortSmall>), dim3((unsigned)grid_for(n, ShortSmall::WPB)),
-                               dim3(ShortSmall::WPB * WAVE), 0, h->stream, r0, n, p.B.cols, Ap, Aj, Ax, Bp, Bj,
-                               Bx, off, cj, cx, alpha, p.row_cnt, l1, cnt, (const int32_t*)nullptr,
-                               (const int32_t*)nullptr, (unsigned long long*)nullptr, (OFF*)nullptr,
-                               (int64_t*)nullptr, (int64_t)0);
+            if (p.use_row && !UB)
+                hipLaunchKernelGGL((k_row<T, IP, OFF, ROW_NUM, RowSmall>), dim3((unsigned)grid_for(n, RowSmall::WPB)),
+                                   dim3(RowSmall::WPB * WAVE), 0, h->stream, r0, n, p.B.cols, Ap, Aj, Ax, Bp, Bj,
+                                   Bx, off, cj, cx, alpha, p.row_cnt, l1, cnt, LbTree{}, (OFF*)nullptr,
+                                   (int64_t*)nullptr, (int64_t)0);
+            else
+                hipLaunchKernelGGL((k_short<T, IP, OFF, MODE, ShortSmall>), dim3((unsigned)grid_for(n, ShortSmall::WPB)),
+                                   dim3(ShortSmall::WPB * WAVE), 0, h->stream, r0, n, p.B.cols, Ap, Aj, Ax, Bp, Bj,
+                                   Bx, off, cj, cx, alpha, p.row_cnt, l1, cnt, (const int32_t*)nullptr,
+                                   (const int32_t*)nullptr, (unsigned long long*)nullptr, (OFF*)nullptr,
+                                   (int64_t*)nullptr, (int64_t)0);
             SPG_LAUNCHED(h);
         }
         if (p.sym_spills == 0) return SPG_STATUS_SUCCESS;
@@ -564,6 +630,38 @@ spg_status_t run_scan(spg_handle_t h, spg_plan_s& p, void* out) {
 template <typename T, typename IP, typename OUT>
 spg_status_t alg1_fused_run(spg_handle_t h, spg_plan_s& p, void* cp) {
     PhaseTimer pt(h, SPG_PHASE_NUMERIC);
+    if (p.use_row && row_lb_enabled()) {
+        LbTree tree;
+        lbt_words(p.A.rows, &tree, p.lb);
+        tree.trace = nullptr;
+        // SPG_LB_TRACE=<file>: per-row wall-clock stamps (start, published, value work done,
+        // base known) of this launch, written as raw uint64 (diagnostics only)
+        const char* trace_path = std::getenv("SPG_LB_TRACE");
+        if (trace_path && p.A.rows > 0) {
+            SPG_HIP(h, hipMalloc((void**)&tree.trace, sizeof(unsigned long long) * 4 * (size_t)p.A.rows));
+            SPG_HIP(h, hipMemsetAsync(tree.trace, 0, sizeof(unsigned long long) * 4 * (size_t)p.A.rows, h->stream));
+        }
+        struct TraceDump {
+            spg_handle_t h; unsigned long long* d; int64_t rows; const char* path;
+            ~TraceDump() {
+                if (!d) return;
+                std::vector<unsigned long long> v((size_t)rows * 4);
+                if (hipMemcpyAsync(v.data(), d, v.size() * 8, hipMemcpyDeviceToHost, h->stream) == hipSuccess &&
+                    hipStreamSynchronize(h->stream) == hipSuccess) {
+                    if (FILE* f = std::fopen(path, "wb")) { std::fwrite(v.data(), 8, v.size(), f); std::fclose(f); }
+                }
+                (void)hipFree(d);
+            }
+        } dump{h, tree.trace, p.A.rows, trace_path};
+        hipLaunchKernelGGL((k_row<T, IP, OUT, ROW_LB, RowSmall>), dim3((unsigned)grid_for(p.A.rows, RowSmall::WPB)),
+                           dim3(RowSmall::WPB * WAVE), 0, h->stream, (int64_t)0, p.A.rows, p.B.cols,
+                           (const IP*)p.A.indptr, (const int32_t*)p.A.indices, (const T*)p.A.values,
+                           (const IP*)p.B.indptr, (const int32_t*)p.B.indices, (const T*)p.B.values,
+                           (const OUT*)nullptr, p.tj, (T*)p.tx, (T)1, p.row_cnt, p.spill,
+                           spill_counts(p, true), tree, (OUT*)cp, p.scalars, p.cap);
+        SPG_LAUNCHED(h);
+        return SPG_STATUS_SUCCESS;
+    }
     hipLaunchKernelGGL((k_short<T, IP, OUT, SHORT_NUMLB, ShortSmall>), dim3((unsigned)grid_for(p.A.rows, ShortSmall::WPB)),
                        dim3(ShortSmall::WPB * WAVE), 0, h->stream, (int64_t)0, p.A.rows, p.B.cols,
                        (const IP*)p.A.indptr, (const int32_t*)p.A.indices, (const T*)p.A.values,
@@ -571,6 +669,19 @@ spg_status_t alg1_fused_run(spg_handle_t h, spg_plan_s& p, void* cp) {
                        (const OUT*)nullptr, p.tj, (T*)p.tx, (T)1, p.row_cnt, (int32_t*)nullptr,
                        (int32_t*)nullptr, (const int32_t*)nullptr, (const int32_t*)nullptr, p.lb, (OUT*)cp,
                        p.scalars, p.cap);
+    SPG_LAUNCHED(h);
+    return SPG_STATUS_SUCCESS;
+}
+
+// ALG1 single pass on k_row: values of the rows it spilled (at the row pointer it wrote)
+template <typename T, typename IP, typename OUT>
+spg_status_t alg1_fused_spills(spg_handle_t h, spg_plan_s& p, const void* cp) {
+    PhaseTimer ps(h, SPG_PHASE_SPILL);
+    hipLaunchKernelGGL((k_numeric<T, IP, OUT, false>), dim3(p.list_grid), dim3(BLOCK), 0, h->stream,
+                       (int64_t)0, p.A.rows, p.B.cols, (const IP*)p.A.indptr, (const int32_t*)p.A.indices,
+                       (const T*)p.A.values, (const IP*)p.B.indptr, (const int32_t*)p.B.indices,
+                       (const T*)p.B.values, (const OUT*)cp, p.tj, (T*)p.tx, (T)1, p.row_cnt, p.seg,
+                       (int64_t)0, p.seg_len, (const int32_t*)p.spill, (const int32_t*)spill_counts(p, true));
     SPG_LAUNCHED(h);
     return SPG_STATUS_SUCCESS;
 }
@@ -754,6 +865,7 @@ spg_status_t spg_plan(spg_handle_t h, const spg_csr_t* A, const spg_csr_t* B, sp
     tmp.cf = chunk_fraction;
     tmp.seg_len = A->nnz;
     tmp.use_short = want_short(*A, *B);
+    tmp.use_row = row_kernel_enabled();
     tmp.use_tile = !tmp.use_short && want_tile(*A, *B, tmp.tws, tmp.G);
     if (tmp.use_tile) {
         tmp.TR = 1;
@@ -883,6 +995,18 @@ spg_status_t spg_symbolic(spg_handle_t h, spg_plan_t p, void* C_indptr, spg_inde
             p->alg1_fused = true;
             const int64_t tot = sc[LB_TOTAL];
             if (C_indptr_type == SPG_INDEX_32I && tot > 2147483647LL) return SPG_STATUS_OVERFLOW;
+            // k_row spilled rows (counted, row pointer written): their values, at that offset
+            if (p->use_row && row_lb_enabled() && (int32_t)(sc[5] & 0xffffffffu) > 0) {
+                st = dispatch_value(p->A.value_type, [&](auto tag) {
+                    using T = decltype(tag);
+                    if (i64)
+                        return C_indptr_type == SPG_INDEX_64I ? alg1_fused_spills<T, int64_t, int64_t>(h, *p, C_indptr)
+                                                              : alg1_fused_spills<T, int64_t, int32_t>(h, *p, C_indptr);
+                    return C_indptr_type == SPG_INDEX_64I ? alg1_fused_spills<T, int32_t, int64_t>(h, *p, C_indptr)
+                                                          : alg1_fused_spills<T, int32_t, int32_t>(h, *p, C_indptr);
+                });
+                if (st) return st;
+            }
             p->nnzC = tot;
             p->c_indptr = C_indptr;
             p->c_indptr_type = C_indptr_type;
