@@ -24,6 +24,7 @@ using namespace spg;
 
 struct spg_handle_s {
     int device = 0;
+    int cus = 256;                  // compute units (persistent grids)
     hipStream_t stream = nullptr;
     int last_hip = 0;
     int64_t* pinned = nullptr;      // 8 host-pinned int64 for device->host scalars
@@ -123,15 +124,6 @@ inline bool row_kernel_enabled() {
     static const bool on = [] {
         const char* e = std::getenv("SPG_SHORT_KERNEL");
         return !(e && std::strcmp(e, "short") == 0);
-    }();
-    return on;
-}
-
-// SPG_ALG1_ROW=1: the ALG1 single pass on k_row's arrival tree (experimental)
-inline bool row_lb_enabled() {
-    static const bool on = [] {
-        const char* e = std::getenv("SPG_ALG1_ROW");
-        return e && std::strcmp(e, "1") == 0;
     }();
     return on;
 }
@@ -353,37 +345,10 @@ inline bool fused_alg1(const spg_plan_s& p) {
     return p.alg == SPG_ALG1 && p.use_short && !p.use_tile && p.A.rows <= (1LL << 24);
 }
 
-// ALG1 single pass on k_row: the 64-ary arrival tree over the rows (spgemm_row.hpp).
-// Words: agg[0] (rows) | agg[1] grp[1] | agg[2] grp[2] | agg[3] grp[3].
-inline size_t lbt_words(int64_t rows, LbTree* t = nullptr, unsigned long long* base = nullptr) {
-    long long n[4] = {rows, 0, 0, 0};
-    int top = 0;
-    while (top < 3 && n[top] > 64) {
-        n[top + 1] = (n[top] + 63) / 64;
-        ++top;
-    }
-    size_t w = (size_t)std::max<long long>(rows, 1);
-    if (t) {
-        t->agg[0] = base;
-        t->grp[0] = nullptr;
-        t->top = top;
-    }
-    for (int lv = 0; lv < 4; ++lv) {
-        if (t) t->n[lv] = n[lv];
-        if (lv == 0 || lv > top) continue;
-        if (t) {
-            t->agg[lv] = base + w;
-            t->grp[lv] = base + w + n[lv];
-        }
-        w += 2 * (size_t)n[lv];
-    }
-    return w;
-}
-
 // status words: products scan | row-pointer scan | item scan (tile path)
 inline size_t status_words(const spg_plan_s& p) {
     return 2 * (size_t)(scan_tiles(p.A.rows) + 1) + (p.use_tile ? (size_t)scan_tiles(tile_items(p)) + 1 : 0) +
-           (fused_alg1(p) ? std::max(lbt_words(p.A.rows), (size_t)grid_for(p.A.rows, ShortSmall::WPB) + 1) : 0);
+           (fused_alg1(p) ? (size_t)grid_for(p.A.rows, ShortSmall::WPB) + 1 : 0);
 }
 inline unsigned long long* item_scan_status(const spg_plan_s& p) {
     return p.scan_status + 2 * (scan_tiles(p.A.rows) + 1);
@@ -520,8 +485,8 @@ spg_status_t run_symbolic_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_
                                    dim3((unsigned)grid_for(n, RowSmall::WPB)), dim3(RowSmall::WPB * WAVE), 0,
                                    h->stream, r0, n, p.B.cols, Ap, Aj, (const double*)nullptr, Bp, Bj,
                                    (const double*)nullptr, (const int64_t*)nullptr, (int32_t*)nullptr,
-                                   (double*)nullptr, 1.0, p.row_cnt, l1, cnt, LbTree{}, (int64_t*)nullptr,
-                                   (int64_t*)nullptr, (int64_t)0);
+                                   (double*)nullptr, 1.0, p.row_cnt, l1, cnt, 0, (int64_t)0,
+                                   (const int64_t*)nullptr);
             else
                 hipLaunchKernelGGL((k_short<double, IP, int64_t, SHORT_SYM, ShortSmall>),
                                    dim3((unsigned)grid_for(n, ShortSmall::WPB)), dim3(ShortSmall::WPB * WAVE), 0,
@@ -578,8 +543,8 @@ spg_status_t run_numeric_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_t
             if (p.use_row && !UB)
                 hipLaunchKernelGGL((k_row<T, IP, OFF, ROW_NUM, RowSmall>), dim3((unsigned)grid_for(n, RowSmall::WPB)),
                                    dim3(RowSmall::WPB * WAVE), 0, h->stream, r0, n, p.B.cols, Ap, Aj, Ax, Bp, Bj,
-                                   Bx, off, cj, cx, alpha, p.row_cnt, l1, cnt, LbTree{}, (OFF*)nullptr,
-                                   (int64_t*)nullptr, (int64_t)0);
+                                   Bx, off, cj, cx, alpha, p.row_cnt, l1, cnt, 0, (int64_t)0,
+                                   (const int64_t*)nullptr);
             else
                 hipLaunchKernelGGL((k_short<T, IP, OFF, MODE, ShortSmall>), dim3((unsigned)grid_for(n, ShortSmall::WPB)),
                                    dim3(ShortSmall::WPB * WAVE), 0, h->stream, r0, n, p.B.cols, Ap, Aj, Ax, Bp, Bj,
@@ -629,39 +594,33 @@ spg_status_t run_scan(spg_handle_t h, spg_plan_s& p, void* out) {
 // ALG1 single pass: structure + values + row pointer in one launch, compact into tj/tx
 template <typename T, typename IP, typename OUT>
 spg_status_t alg1_fused_run(spg_handle_t h, spg_plan_s& p, void* cp) {
-    PhaseTimer pt(h, SPG_PHASE_NUMERIC);
-    if (p.use_row && row_lb_enabled()) {
-        LbTree tree;
-        lbt_words(p.A.rows, &tree, p.lb);
-        tree.trace = nullptr;
-        // SPG_LB_TRACE=<file>: per-row wall-clock stamps (start, published, value work done,
-        // base known) of this launch, written as raw uint64 (diagnostics only)
-        const char* trace_path = std::getenv("SPG_LB_TRACE");
-        if (trace_path && p.A.rows > 0) {
-            SPG_HIP(h, hipMalloc((void**)&tree.trace, sizeof(unsigned long long) * 4 * (size_t)p.A.rows));
-            SPG_HIP(h, hipMemsetAsync(tree.trace, 0, sizeof(unsigned long long) * 4 * (size_t)p.A.rows, h->stream));
+    if (p.use_row) {
+        // count pass (every row), row-pointer scan, one numeric pass into C's compact
+        // arrays (estimate-sized: a total past `cap` writes nothing and is redone)
+        const unsigned grid = (unsigned)grid_for(p.A.rows, RowSmall::WPB);
+        if (!p.counts_ready) {
+            PhaseTimer ps(h, SPG_PHASE_SYMBOLIC);
+            hipLaunchKernelGGL((k_row<double, IP, OUT, ROW_SYM, RowSmall>), dim3(grid), dim3(RowSmall::WPB * WAVE), 0,
+                               h->stream, (int64_t)0, p.A.rows, p.B.cols, (const IP*)p.A.indptr,
+                               (const int32_t*)p.A.indices, (const double*)nullptr, (const IP*)p.B.indptr,
+                               (const int32_t*)p.B.indices, (const double*)nullptr, (const OUT*)nullptr,
+                               (int32_t*)nullptr, (double*)nullptr, 1.0, p.row_cnt, p.spill,
+                               spill_counts(p, true), (int)ROW_COUNT_ALL, (int64_t)0, (const int64_t*)nullptr);
+            SPG_LAUNCHED(h);
         }
-        struct TraceDump {
-            spg_handle_t h; unsigned long long* d; int64_t rows; const char* path;
-            ~TraceDump() {
-                if (!d) return;
-                std::vector<unsigned long long> v((size_t)rows * 4);
-                if (hipMemcpyAsync(v.data(), d, v.size() * 8, hipMemcpyDeviceToHost, h->stream) == hipSuccess &&
-                    hipStreamSynchronize(h->stream) == hipSuccess) {
-                    if (FILE* f = std::fopen(path, "wb")) { std::fwrite(v.data(), 8, v.size(), f); std::fclose(f); }
-                }
-                (void)hipFree(d);
-            }
-        } dump{h, tree.trace, p.A.rows, trace_path};
-        hipLaunchKernelGGL((k_row<T, IP, OUT, ROW_LB, RowSmall>), dim3((unsigned)grid_for(p.A.rows, RowSmall::WPB)),
-                           dim3(RowSmall::WPB * WAVE), 0, h->stream, (int64_t)0, p.A.rows, p.B.cols,
-                           (const IP*)p.A.indptr, (const int32_t*)p.A.indices, (const T*)p.A.values,
-                           (const IP*)p.B.indptr, (const int32_t*)p.B.indices, (const T*)p.B.values,
-                           (const OUT*)nullptr, p.tj, (T*)p.tx, (T)1, p.row_cnt, p.spill,
-                           spill_counts(p, true), tree, (OUT*)cp, p.scalars, p.cap);
+        spg_status_t st = run_scan<OUT>(h, p, cp);
+        if (st) return st;
+        PhaseTimer pn(h, SPG_PHASE_NUMERIC);
+        hipLaunchKernelGGL((k_row<T, IP, OUT, ROW_NUM, RowSmall>), dim3(grid), dim3(RowSmall::WPB * WAVE), 0,
+                           h->stream, (int64_t)0, p.A.rows, p.B.cols, (const IP*)p.A.indptr,
+                           (const int32_t*)p.A.indices, (const T*)p.A.values, (const IP*)p.B.indptr,
+                           (const int32_t*)p.B.indices, (const T*)p.B.values, (const OUT*)cp, p.tj, (T*)p.tx,
+                           (T)1, p.row_cnt, p.spill, spill_counts(p, true), (int)ROW_LISTED,
+                           std::max<int64_t>(p.cap, 1), (const int64_t*)p.scalars);
         SPG_LAUNCHED(h);
         return SPG_STATUS_SUCCESS;
     }
+    PhaseTimer pt(h, SPG_PHASE_NUMERIC);
     hipLaunchKernelGGL((k_short<T, IP, OUT, SHORT_NUMLB, ShortSmall>), dim3((unsigned)grid_for(p.A.rows, ShortSmall::WPB)),
                        dim3(ShortSmall::WPB * WAVE), 0, h->stream, (int64_t)0, p.A.rows, p.B.cols,
                        (const IP*)p.A.indptr, (const int32_t*)p.A.indices, (const T*)p.A.values,
@@ -810,6 +769,7 @@ spg_status_t spg_create(spg_handle_t* handle, int hip_device) {
     spg_handle_s* h = new (std::nothrow) spg_handle_s();
     if (!h) return SPG_STATUS_ALLOC_FAILED;
     h->device = dev;
+    h->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     hipError_t e = hipSetDevice(dev);
     if (e == hipSuccess) e = hipHostMalloc((void**)&h->pinned, 16 * sizeof(int64_t), hipHostMallocDefault);
     if (e != hipSuccess) {
@@ -961,6 +921,56 @@ spg_status_t spg_symbolic(spg_handle_t h, spg_plan_t p, void* C_indptr, spg_inde
     SPG_HIP(h, hipSetDevice(h->device));
     spg_status_t st;
     const bool i64 = p->A.indptr_type == SPG_INDEX_64I;
+    if (fused_alg1(*p) && !p->fused_failed && p->use_row) {
+        // ALG1 on k_row: count pass (first call only), row-pointer scan, numeric pass into
+        // the workspace's compact C -- no host sync in between.  A repeated call (the int64
+        // retry after an int32 overflow, when the numeric pass wrote nothing) redoes the
+        // scan and the numeric pass.
+        if (p->counts_ready) {
+            const int64_t tiles = scan_tiles(p->A.rows) + 1;
+            SPG_HIP(h, hipMemsetAsync(p->scan_status + tiles, 0, sizeof(unsigned long long) * tiles, h->stream));
+        }
+        st = dispatch_value(p->A.value_type, [&](auto tag) {
+            using T = decltype(tag);
+            return i64 ? alg1_fused_typed<T, int64_t>(h, *p, C_indptr, C_indptr_type)
+                       : alg1_fused_typed<T, int32_t>(h, *p, C_indptr, C_indptr_type);
+        });
+        if (st) return st;
+        p->counts_ready = true;
+        int64_t sc[6];
+        if ((st = read_scalars(h, p->scalars, 6, sc))) return st;
+        if (sc[1]) return SPG_STATUS_OVERFLOW;   // int32 row pointer: retry with int64
+        if (sc[0] <= p->cap) {
+            p->alg1_fused = true;
+            if ((int32_t)(sc[5] & 0xffffffffu) > 0) {   // the listed rows' values, at Cp
+                st = dispatch_value(p->A.value_type, [&](auto tag) {
+                    using T = decltype(tag);
+                    if (i64)
+                        return C_indptr_type == SPG_INDEX_64I ? alg1_fused_spills<T, int64_t, int64_t>(h, *p, C_indptr)
+                                                              : alg1_fused_spills<T, int64_t, int32_t>(h, *p, C_indptr);
+                    return C_indptr_type == SPG_INDEX_64I ? alg1_fused_spills<T, int32_t, int64_t>(h, *p, C_indptr)
+                                                          : alg1_fused_spills<T, int32_t, int32_t>(h, *p, C_indptr);
+                });
+                if (st) return st;
+            }
+            p->nnzC = sc[0];
+            p->c_indptr = C_indptr;
+            p->c_indptr_type = C_indptr_type;
+            *nnzC = sc[0];
+            return SPG_STATUS_SUCCESS;
+        }
+        // an output larger than the estimate: redo the numeric pass into C (the counts and
+        // the row pointer are valid)
+        p->fused_failed = true;
+        p->symbolic_runs = 1;
+        p->sym_spills = (int64_t)(uint32_t)(sc[5] & 0xffffffffu);   // the numeric pass relists them
+        SPG_HIP(h, hipMemsetAsync(spill_counts(*p, true), 0, sizeof(int32_t), h->stream));
+        p->nnzC = sc[0];
+        p->c_indptr = C_indptr;
+        p->c_indptr_type = C_indptr_type;
+        *nnzC = sc[0];
+        return SPG_STATUS_SUCCESS;
+    }
     if (fused_alg1(*p) && !p->fused_failed) {
         // ALG1 single pass: one launch writes C compact into tj/tx and its row pointer; a
         // repeated call (int64 retry) only rescans the row counts it recorded
@@ -996,7 +1006,7 @@ spg_status_t spg_symbolic(spg_handle_t h, spg_plan_t p, void* C_indptr, spg_inde
             const int64_t tot = sc[LB_TOTAL];
             if (C_indptr_type == SPG_INDEX_32I && tot > 2147483647LL) return SPG_STATUS_OVERFLOW;
             // k_row spilled rows (counted, row pointer written): their values, at that offset
-            if (p->use_row && row_lb_enabled() && (int32_t)(sc[5] & 0xffffffffu) > 0) {
+            if (p->use_row && (int32_t)(sc[5] & 0xffffffffu) > 0) {
                 st = dispatch_value(p->A.value_type, [&](auto tag) {
                     using T = decltype(tag);
                     if (i64)

@@ -236,9 +236,9 @@ def test_validate_csr():
 
 
 def test_short_kernel_long_rows():
-    """Rows the short-row kernel keeps but cannot hold in registers: more than 512 products
-    with more than 512 output entries (in-kernel column windows) and with heavy column
-    overlap (many products per output entry)."""
+    """Rows beyond the short-row kernel's register path: more than 640 products (with more
+    than 512 output entries, and with heavy column overlap), and rows whose repeated
+    columns overflow its fix-up list -- all handed to the general kernel, same bits."""
     rng = np.random.default_rng(21)
     cases = [
         (sp.random(200, 2000, density=0.02, format="csr", random_state=rng),
@@ -247,6 +247,10 @@ def test_short_kernel_long_rows():
          sp.random(2000, 300, density=0.05, format="csr", random_state=rng)),    # P~900, nnz<=300
         (sp.random(100, 3000, density=0.02, format="csr", random_state=rng),
          sp.random(3000, 16384, density=0.01, format="csr", random_state=rng)),  # widest short case
+        # ~350 products into 200 columns: k_row's list of products in flagged (repeated)
+        # bitmap words overflows 64 entries -> the general kernel, in every algorithm
+        (sp.random(1000, 2000, density=0.0175, format="csr", random_state=rng),
+         sp.random(2000, 200, density=0.05, format="csr", random_state=rng)),
     ]
     for A, B in cases:
         A.sort_indices(); B.sort_indices()
