@@ -196,6 +196,24 @@ spg_status_t spg_validate_csr(spg_handle_t handle, const spg_csr_t *M, int *is_c
  * caller's workspace. */
 spg_status_t spg_plan_destroy(spg_plan_t plan);
 
+/* The whole call sequence of cupyx.cusparse.spgemm (cupy-src/cupyx/cusparse.py:2041-2142:
+ * workEstimation/estimateMemory -> compute -> getSize -> copy) in ONE call, for a caller
+ * that holds the workspace spg_plan's size query asked for (same A, B, alg,
+ * chunk_fraction).  Writes C's row pointer (rows(A)+1 entries of C_indptr_type;
+ * SPG_STATUS_OVERFLOW when int32 cannot hold nnz(C): call again with an int64 array) and
+ * nnz(C) to *nnzC (the call's one host sync).
+ *   When C's columns and values sit compact in the workspace (ALG1), they are scaled by
+ *   *alpha in place, *C_indices / *C_values point at them (nnzC entries) and *plan_out is
+ *   NULL: the product is complete (stream-ordered).
+ *   Otherwise *C_indices / *C_values are NULL and *plan_out is the live plan: the caller
+ *   allocates C's arrays (nnzC entries) and finishes with spg_numeric + spg_plan_destroy.
+ * *peak_bytes is the spg_peak_bytes figure for this product.  No cuSPARSE counterpart: it
+ * removes four host round trips per product from a binding's call path. */
+spg_status_t spg_spgemm_ws(spg_handle_t handle, const spg_csr_t *A, const spg_csr_t *B, spg_alg_t alg,
+                           float chunk_fraction, const void *alpha, void *workspace, size_t workspace_bytes,
+                           void *C_indptr, spg_index_t C_indptr_type, int64_t *nnzC, void **C_indices,
+                           void **C_values, size_t *peak_bytes, spg_plan_t *plan_out);
+
 /* Per-phase device timing: with timing enabled every kernel the handle launches is
  * bracketed by hipEvents on the handle's stream, and spg_get_timing returns the
  * accumulated device milliseconds and launch counts per phase (the build's equivalent of

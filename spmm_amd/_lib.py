@@ -43,7 +43,8 @@ STATUS_OVERFLOW = 100
 EXPORTS = ("spg_version", "spg_status_string", "spg_create", "spg_destroy", "spg_set_stream",
            "spg_last_hip_error", "spg_plan", "spg_num_products", "spg_symbolic",
            "spg_numeric", "spg_peak_bytes", "spg_validate_csr", "spg_plan_destroy",
-           "spg_set_timing", "spg_get_timing", "spg_result_in_workspace", "spg_spmv")
+           "spg_set_timing", "spg_get_timing", "spg_result_in_workspace", "spg_spmv",
+           "spg_spgemm_ws")
 
 PHASES = ("products", "scan", "symbolic", "numeric", "compact", "validate", "spill", "spmv")
 NUM_PHASES = 8
@@ -107,6 +108,9 @@ def load():
             "spg_peak_bytes": (ctypes.c_int, [vp, ctypes.POINTER(sz)]),
             "spg_validate_csr": (ctypes.c_int, [vp, csrp, ctypes.POINTER(ctypes.c_int)]),
             "spg_plan_destroy": (ctypes.c_int, [vp]),
+            "spg_spgemm_ws": (ctypes.c_int, [vp, csrp, csrp, ctypes.c_int, ctypes.c_float, vp, vp, sz, vp,
+                                             ctypes.c_int, ctypes.POINTER(i64), ctypes.POINTER(vp),
+                                             ctypes.POINTER(vp), ctypes.POINTER(sz), ctypes.POINTER(vp)]),
             "spg_set_timing": (ctypes.c_int, [vp, ctypes.c_int]),
             "spg_get_timing": (ctypes.c_int, [vp, ctypes.POINTER(SpgTiming)]),
         }
@@ -135,7 +139,10 @@ class Handle:
         self.ptr = h
 
     def set_stream(self, stream_ptr: int) -> None:
+        if stream_ptr == getattr(self, "_stream", None):
+            return
         check(self.lib.spg_set_stream(self.ptr, ctypes.c_void_p(stream_ptr)), "spg_set_stream")
+        self._stream = stream_ptr
 
     def set_timing(self, enable: bool) -> None:
         check(self.lib.spg_set_timing(self.ptr, int(enable)), "spg_set_timing")

@@ -1158,6 +1158,41 @@ spg_status_t spg_plan_destroy(spg_plan_t p) {
     return SPG_STATUS_SUCCESS;
 }
 
+spg_status_t spg_spgemm_ws(spg_handle_t h, const spg_csr_t* A, const spg_csr_t* B, spg_alg_t alg,
+                           float chunk_fraction, const void* alpha, void* workspace, size_t workspace_bytes,
+                           void* C_indptr, spg_index_t C_indptr_type, int64_t* nnzC, void** C_indices,
+                           void** C_values, size_t* peak_bytes, spg_plan_t* plan_out) {
+    if (!h) return SPG_STATUS_NOT_INITIALIZED;
+    if (!alpha || !nnzC || !C_indices || !C_values || !peak_bytes || !plan_out) return SPG_STATUS_INVALID_VALUE;
+    *plan_out = nullptr;
+    *C_indices = *C_values = nullptr;
+    spg_plan_t p = nullptr;
+    size_t wsb = workspace_bytes;
+    spg_status_t st = spg_plan(h, A, B, alg, chunk_fraction, &wsb, workspace, &p);
+    if (st) return st;
+    if ((st = spg_symbolic(h, p, C_indptr, C_indptr_type, nnzC))) {
+        spg_plan_destroy(p);
+        return st;
+    }
+    const size_t ipc = C_indptr_type == SPG_INDEX_32I ? 4 : 8;
+    if (p->alg1_fused && *nnzC > 0) {
+        // C already compact in the workspace: scale in place (alpha != 1) and finish
+        spg_csr_t C{p->A.rows, p->B.cols, *nnzC, C_indptr, p->tj, p->tx, C_indptr_type, p->A.value_type};
+        st = spg_numeric(h, p, alpha, &C);
+        if (!st) {
+            *C_indices = p->tj;
+            *C_values = p->tx;
+            *peak_bytes = p->ws_bytes + ipc * (size_t)(p->A.rows + 1);
+        }
+        spg_plan_destroy(p);
+        return st;
+    }
+    *peak_bytes = p->ws_bytes + ipc * (size_t)(p->A.rows + 1) +
+                  (size_t)*nnzC * (sizeof(int32_t) + vbytes(p->A.value_type));
+    *plan_out = p;   // the caller allocates C's arrays, then spg_numeric + spg_plan_destroy
+    return SPG_STATUS_SUCCESS;
+}
+
 spg_status_t spg_set_timing(spg_handle_t h, int enable) {
     if (!h) return SPG_STATUS_NOT_INITIALIZED;
     SPG_HIP(h, hipStreamSynchronize(h->stream));

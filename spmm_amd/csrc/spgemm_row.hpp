@@ -384,11 +384,9 @@ __device__ int row_count_only(Lds& S, int l, int64_t a0, int nA, const int32_t* 
 //     count pass listed them).  cap > 0 (ALG1, C's arrays hold `cap` entries): a row that
 //     would end past cap writes nothing (the host sees the total and redoes the product).
 enum { ROW_COUNT_ALL = 1, ROW_LISTED = 2 };
-#ifndef SPG_ROW_WAVES
-#define SPG_ROW_WAVES 1   // minimum waves per SIMD k_row is compiled for (register budget)
-#endif
+// register budget: 5 waves per SIMD (<= 96 VGPRs) for 4- and 8-byte values
 template <typename T, typename IP, typename OFF, int MODE, typename G>
-__global__ __launch_bounds__(G::WPB * WAVE, SPG_ROW_WAVES) void k_row(
+__global__ __launch_bounds__(G::WPB * WAVE, sizeof(T) <= 8 ? 5 : 3) void k_row(
     int64_t row0, int64_t nrows, int64_t ncols, const IP* __restrict__ Ap,
     const int32_t* __restrict__ Aj, const T* __restrict__ Ax, const IP* __restrict__ Bp,
     const int32_t* __restrict__ Bj, const T* __restrict__ Bx, const OFF* __restrict__ Coff,

@@ -144,58 +144,48 @@ def spgemm(a, b, alpha=1, alg=0, chunk_fraction=0.2, verbose=False):
     h = _handle_for(a)
     lib = h.lib
     va, vb = _csr_view(a), _csr_view(b)
+    cf = float(chunk_fraction)
     ws_bytes = ctypes.c_size_t(0)
-    check(lib.spg_plan(h.ptr, ctypes.byref(va), ctypes.byref(vb), algo, float(chunk_fraction),
+    check(lib.spg_plan(h.ptr, ctypes.byref(va), ctypes.byref(vb), algo, cf,
                        ctypes.byref(ws_bytes), None, None), "spg_plan")
     if verbose:
         print("USING ALG", alg, "workspace GB =", ws_bytes.value / (1024 ** 3))
+    # workspace from torch's caching allocator on the current stream (the library works on
+    # that stream, so a later reuse of the block is ordered after this product)
     ws = torch.empty(max(ws_bytes.value, 1), dtype=torch.uint8, device=dev)
-    plan = ctypes.c_void_p()
-    check(lib.spg_plan(h.ptr, ctypes.byref(va), ctypes.byref(vb), algo, float(chunk_fraction),
-                       ctypes.byref(ws_bytes), ctypes.c_void_p(ws.data_ptr()),
-                       ctypes.byref(plan)), "spg_plan")
-    try:
-        indptr = torch.empty(m + 1, dtype=torch.int32, device=dev)
-        nnz = ctypes.c_int64(0)
-        st = lib.spg_symbolic(h.ptr, plan, ctypes.c_void_p(indptr.data_ptr()),
-                              _lib.SPG_INDEX_32I, ctypes.byref(nnz))
-        if st == _lib.STATUS_OVERFLOW:      # nnz(C) >= 2**31: redo the scan into int64
-            indptr = torch.empty(m + 1, dtype=torch.int64, device=dev)
-            st = lib.spg_symbolic(h.ptr, plan, ctypes.c_void_p(indptr.data_ptr()),
-                                  _lib.SPG_INDEX_64I, ctypes.byref(nnz))
-        check(st, "spg_symbolic")
-        nnzc = int(nnz.value)
-        # ALG1 single pass: C already sits compact in the workspace -- take views of it
-        pj, px = ctypes.c_void_p(), ctypes.c_void_p()
-        check(lib.spg_result_in_workspace(plan, ctypes.byref(pj), ctypes.byref(px)),
-              "spg_result_in_workspace")
-        in_ws = bool(pj.value) and nnzc > 0
-        if in_ws:
-            base = ws.data_ptr()
-            vsz = a.data.element_size()
-            oj, ox = pj.value - base, px.value - base
-            indices = ws[oj:oj + 4 * nnzc].view(torch.int32)
-            data = ws[ox:ox + vsz * nnzc].view(a.data.dtype)
-        else:
+    ct, nparts = _ALPHA_CT[a.data.dtype]
+    al = (ct * 2)(complex(alpha).real, complex(alpha).imag) if nparts == 2 else ct(float(alpha))
+    nnz, peak = ctypes.c_int64(0), ctypes.c_size_t(0)
+    pj, px, plan = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+    # plan -> symbolic (nnz(C) to the host) -> numeric in one call (spg_spgemm_ws)
+    for it in (torch.int32, torch.int64):   # int64 row pointer once nnz(C) >= 2**31
+        indptr = torch.empty(m + 1, dtype=it, device=dev)
+        st = lib.spg_spgemm_ws(h.ptr, ctypes.byref(va), ctypes.byref(vb), algo, cf, ctypes.byref(al),
+                               ctypes.c_void_p(ws.data_ptr()), ws_bytes.value,
+                               ctypes.c_void_p(indptr.data_ptr()), _IT[it], ctypes.byref(nnz),
+                               ctypes.byref(pj), ctypes.byref(px), ctypes.byref(peak), ctypes.byref(plan))
+        if st != _lib.STATUS_OVERFLOW:
+            break
+    check(st, "spg_spgemm_ws")
+    nnzc = int(nnz.value)
+    if pj.value:
+        # ALG1: C sits compact (scaled) in the workspace -- views of it
+        base = ws.data_ptr()
+        oj, ox = pj.value - base, px.value - base
+        indices = ws[oj:oj + 4 * nnzc].view(torch.int32)
+        data = ws[ox:ox + a.data.element_size() * nnzc].view(a.data.dtype)
+    else:
+        try:
             indices = torch.empty(nnzc, dtype=torch.int32, device=dev)
             data = torch.empty(nnzc, dtype=a.data.dtype, device=dev)
-        c = csr_matrix._from_parts(data, indices, indptr, (m, n), canonical=True)
-        vc = SpgCsr(m, n, nnzc, indptr.data_ptr(), indices.data_ptr() if nnzc else 0,
-                    data.data_ptr() if nnzc else 0, _IT[indptr.dtype], _VT[data.dtype])
-        ct, nparts = _ALPHA_CT[a.data.dtype]
-        al = (ct * 2)(complex(alpha).real, complex(alpha).imag) if nparts == 2 else ct(float(alpha))
-        check(lib.spg_numeric(h.ptr, plan, ctypes.byref(al), ctypes.byref(vc)), "spg_numeric")
-        peak = ctypes.c_size_t(0)
-        lib.spg_peak_bytes(plan, ctypes.byref(peak))
-        if in_ws:   # C's arrays are views of the workspace: workspace + row pointer
-            peak = ctypes.c_size_t(int(ws_bytes.value) + indptr.element_size() * (m + 1))
-        last_stats.alg, last_stats.workspace_bytes = int(algo), int(ws_bytes.value)
-        last_stats.peak_bytes, last_stats.nnz = int(peak.value), nnzc
-        # keep the workspace alive until the queued kernels have consumed it
-        ws.record_stream(torch.cuda.current_stream(dev))
-        return c
-    finally:
-        lib.spg_plan_destroy(plan)
+            vc = SpgCsr(m, n, nnzc, indptr.data_ptr(), indices.data_ptr() if nnzc else 0,
+                        data.data_ptr() if nnzc else 0, _IT[indptr.dtype], _VT[data.dtype])
+            check(lib.spg_numeric(h.ptr, plan, ctypes.byref(al), ctypes.byref(vc)), "spg_numeric")
+        finally:
+            lib.spg_plan_destroy(plan)
+    last_stats.alg, last_stats.workspace_bytes = int(algo), int(ws_bytes.value)
+    last_stats.peak_bytes, last_stats.nnz = int(peak.value), nnzc
+    return csr_matrix._from_parts(data, indices, indptr, (m, n), canonical=True)
 
 
 def spmv(a, x, y=None, alpha=1, beta=0, transa=False):
