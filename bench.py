@@ -13,7 +13,7 @@ plan, symbolic with its nnz(C) host sync, C allocation, numeric), inputs residen
   the step), every rank computes its C slab; no collective inside the step.
   value = sum over ranks of 2*P_r per step / max-over-ranks step time.
 
-Also reported: ``roofline`` for the numeric-phase kernel (k_short here; algorithmic bytes per
+Also reported: ``roofline`` for the numeric-phase kernel (k_row here; algorithmic bytes per
 launch / its average device time from HIP events on the library's stream, SURVEY 8d
 compulsory-bytes model) and ``cpu_baseline`` (the oracle's C restatement of scipy's
 csr_matmat, single thread, on the same A and B, rank 0 at N=1), plus scipy itself.
@@ -161,7 +161,7 @@ def main():
     dom = max(phases.items(), key=lambda kv: kv[1][0])
     avgA, avgB = A.nnz / max(A.shape[0], 1), B.nnz / max(B.shape[0], 1)
     # which kernel the numeric phase launches (the library's own dispatch rule, want_short)
-    num_kernel = ("k_short" if B.shape[1] <= 16384 and avgA <= 48 and avgA * avgB <= 400
+    num_kernel = ("k_row" if B.shape[1] <= 16384 and avgA <= 48 and avgA * avgB <= 400
                   else "k_tile / k_numeric")
     dom_name, (dom_ms, dom_launches) = dom
     num_ms, num_launches = phases["numeric"]

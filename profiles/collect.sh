@@ -19,5 +19,5 @@ timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/prof" 
     -- python3 bench.py $ARGS --steps 5 --warmup 2 --cpu-seconds 0 > "$OUT/prof_write.log" 2>&1
 python3 profiles/summarize.py "$OUT/prof" > "$OUT/summary_${ROUND}.txt"
 KEY=${PMC_KEY:-n16384_d0.001_float64_alg1}
-python3 profiles/pmc_to_json.py "$OUT/prof" "$KEY" "${PMC_KERNEL:-k_short<double, int, int, 3}" "$OUT/pmc_traffic.json"
+python3 profiles/pmc_to_json.py "$OUT/prof" "$KEY" "${PMC_KERNEL:-k_row<double, int, int, 1}" "$OUT/pmc_traffic.json"
 echo "collect done ($ROUND)"

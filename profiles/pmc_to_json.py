@@ -21,12 +21,18 @@ import sys
 
 
 def per_launch(d, counter, rx):
-    vals = []
+    """Average over the matching dispatches with the LARGEST grid (the full product; ALG3's
+    row chunks launch the same kernel on smaller grids)."""
+    rows = []
     for f in glob.glob(os.path.join(d, "*counter_collection.csv")):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] == counter and rx.search(r["Kernel_Name"]):
-                vals.append(float(r["Counter_Value"]))
-    return (sum(vals) / len(vals), len(vals)) if vals else (None, 0)
+                rows.append((int(r["Grid_Size"]), float(r["Counter_Value"])))
+    if not rows:
+        return None, 0
+    g = max(x[0] for x in rows)
+    vals = [v for gs, v in rows if gs == g]
+    return sum(vals) / len(vals), len(vals)
 
 
 def main():

@@ -14,6 +14,17 @@ def short(name):
 
 
 def main(d):
+    # per (kernel, grid): average duration from the per-dispatch trace
+    for f in sorted(glob.glob(os.path.join(d, "*kernel_trace.csv"))):
+        print(f"== {os.path.basename(f)} (per kernel and grid size)")
+        acc = defaultdict(list)
+        for r in csv.DictReader(open(f)):
+            dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+            acc[(short(r["Kernel_Name"]), int(r["Grid_Size_X"]))].append(dur)
+        for (k, g), v in sorted(acc.items(), key=lambda kv: -sum(kv[1])):
+            v.sort()
+            print(f"  {k:55s} grid={g:>9} calls={len(v):>5} avg_us={sum(v)/len(v):8.2f} "
+                  f"median_us={v[len(v)//2]:8.2f}")
     for f in sorted(glob.glob(os.path.join(d, "*kernel_stats.csv"))):
         print(f"== {os.path.basename(f)}")
         for r in csv.DictReader(open(f)):
@@ -23,10 +34,10 @@ def main(d):
         print(f"== {os.path.basename(f)}")
         acc = defaultdict(lambda: defaultdict(list))
         for r in csv.DictReader(open(f)):
-            acc[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
-        for k, cs in acc.items():
+            acc[(short(r["Kernel_Name"]), int(r["Grid_Size"]))][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        for (k, g), cs in sorted(acc.items()):
             vals = "  ".join(f"{c}={sum(v)/len(v):.4g}" for c, v in sorted(cs.items()))
-            print(f"  {k:50s} {vals}")
+            print(f"  {k:50s} grid={g:>9} {vals}")
 
 
 if __name__ == "__main__":

@@ -28,6 +28,8 @@ struct spg_handle_s {
     hipStream_t stream = nullptr;
     int last_hip = 0;
     int64_t* pinned = nullptr;      // 8 host-pinned int64 for device->host scalars
+    int32_t* spill_ctr = nullptr;   // ALG1 on k_row: spill counter, re-armed by the scan kernel
+    bool spill_ctr_dirty = false;   // a count pass ran without its scan (re-zero first)
     void* scratch = nullptr;        // internal device scratch (plan-time analysis)
     size_t scratch_bytes = 0;
     // per-phase timing (spg_set_timing / spg_get_timing)
@@ -252,13 +254,14 @@ spg_status_t ensure_scratch(spg_handle_t h, size_t bytes) {
 // `status` (tiles + 1 words) must be zero: plans zero theirs once when they are built
 template <typename OUT>
 spg_status_t launch_scan(spg_handle_t h, int64_t n, const int64_t* in, OUT* out,
-                         unsigned long long* status, int64_t* scal, bool zero_status) {
+                         unsigned long long* status, int64_t* scal, bool zero_status,
+                         int32_t* move_cnt = nullptr, int64_t* move_dst = nullptr) {
     const int64_t tiles = scan_tiles(n);
     if (zero_status)
         SPG_HIP(h, hipMemsetAsync(status, 0, sizeof(unsigned long long) * (size_t)(tiles + 1), h->stream));
     PhaseTimer pt(h, SPG_PHASE_SCAN);
     hipLaunchKernelGGL(k_scan_lb<OUT>, dim3((unsigned)tiles), dim3(BLOCK), 0, h->stream, n, in, out,
-                       status, scal);
+                       status, scal, move_cnt, move_dst);
     SPG_LAUNCHED(h);
     return SPG_STATUS_SUCCESS;
 }
@@ -482,7 +485,7 @@ spg_status_t run_symbolic_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_
             PhaseTimer pt(h, SPG_PHASE_SYMBOLIC);
             if (p.use_row)
                 hipLaunchKernelGGL((k_row<double, IP, int64_t, ROW_SYM, RowSmall>),
-                                   dim3((unsigned)grid_for(n, RowSmall::WPB)), dim3(RowSmall::WPB * WAVE), 0,
+                                   dim3((unsigned)grid_for(n, RowSmall::WPB * ROW_PAIR)), dim3(RowSmall::WPB * WAVE), 0,
                                    h->stream, r0, n, p.B.cols, Ap, Aj, (const double*)nullptr, Bp, Bj,
                                    (const double*)nullptr, (const int64_t*)nullptr, (int32_t*)nullptr,
                                    (double*)nullptr, 1.0, p.row_cnt, l1, cnt, 0, (int64_t)0,
@@ -541,7 +544,7 @@ spg_status_t run_numeric_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_t
         {
             PhaseTimer pt(h, SPG_PHASE_NUMERIC);
             if (p.use_row && !UB)
-                hipLaunchKernelGGL((k_row<T, IP, OFF, ROW_NUM, RowSmall>), dim3((unsigned)grid_for(n, RowSmall::WPB)),
+                hipLaunchKernelGGL((k_row<T, IP, OFF, ROW_NUM, RowSmall>), dim3((unsigned)grid_for(n, RowSmall::WPB * ROW_PAIR)),
                                    dim3(RowSmall::WPB * WAVE), 0, h->stream, r0, n, p.B.cols, Ap, Aj, Ax, Bp, Bj,
                                    Bx, off, cj, cx, alpha, p.row_cnt, l1, cnt, 0, (int64_t)0,
                                    (const int64_t*)nullptr);
@@ -597,19 +600,33 @@ spg_status_t alg1_fused_run(spg_handle_t h, spg_plan_s& p, void* cp) {
     if (p.use_row) {
         // count pass (every row), row-pointer scan, one numeric pass into C's compact
         // arrays (estimate-sized: a total past `cap` writes nothing and is redone)
-        const unsigned grid = (unsigned)grid_for(p.A.rows, RowSmall::WPB);
+        // no memset of the control block: the count pass zeroes the scan's status words,
+        // spills are counted in the handle's counter, which the scan moves into
+        // scalars[5] and re-arms
+        const unsigned grid = (unsigned)grid_for(p.A.rows, RowSmall::WPB * ROW_PAIR);
+        unsigned long long* status = p.scan_status + scan_tiles(p.A.rows) + 1;
+        const int64_t nstatus = scan_tiles(p.A.rows) + 1;
         if (!p.counts_ready) {
+            if (h->spill_ctr_dirty) SPG_HIP(h, hipMemsetAsync(h->spill_ctr, 0, sizeof(int32_t), h->stream));
+            h->spill_ctr_dirty = true;
             PhaseTimer ps(h, SPG_PHASE_SYMBOLIC);
             hipLaunchKernelGGL((k_row<double, IP, OUT, ROW_SYM, RowSmall>), dim3(grid), dim3(RowSmall::WPB * WAVE), 0,
                                h->stream, (int64_t)0, p.A.rows, p.B.cols, (const IP*)p.A.indptr,
                                (const int32_t*)p.A.indices, (const double*)nullptr, (const IP*)p.B.indptr,
                                (const int32_t*)p.B.indices, (const double*)nullptr, (const OUT*)nullptr,
-                               (int32_t*)nullptr, (double*)nullptr, 1.0, p.row_cnt, p.spill,
-                               spill_counts(p, true), (int)ROW_COUNT_ALL, (int64_t)0, (const int64_t*)nullptr);
+                               (int32_t*)nullptr, (double*)nullptr, 1.0, p.row_cnt, p.spill, h->spill_ctr,
+                               (int)ROW_COUNT_ALL, (int64_t)0, (const int64_t*)nullptr, status, nstatus);
             SPG_LAUNCHED(h);
+            spg_status_t st = launch_scan<OUT>(h, p.A.rows, (const int64_t*)p.row_cnt, (OUT*)cp, status,
+                                               p.scalars, false, h->spill_ctr, p.scalars + 5);
+            if (st) return st;
+            h->spill_ctr_dirty = false;
+        } else {   // repeated call: the first scan already moved the spill count
+            SPG_HIP(h, hipMemsetAsync(status, 0, sizeof(unsigned long long) * (size_t)nstatus, h->stream));
+            spg_status_t st = launch_scan<OUT>(h, p.A.rows, (const int64_t*)p.row_cnt, (OUT*)cp, status,
+                                               p.scalars, false);
+            if (st) return st;
         }
-        spg_status_t st = run_scan<OUT>(h, p, cp);
-        if (st) return st;
         PhaseTimer pn(h, SPG_PHASE_NUMERIC);
         hipLaunchKernelGGL((k_row<T, IP, OUT, ROW_NUM, RowSmall>), dim3(grid), dim3(RowSmall::WPB * WAVE), 0,
                            h->stream, (int64_t)0, p.A.rows, p.B.cols, (const IP*)p.A.indptr,
@@ -640,7 +657,7 @@ spg_status_t alg1_fused_spills(spg_handle_t h, spg_plan_s& p, const void* cp) {
                        (int64_t)0, p.A.rows, p.B.cols, (const IP*)p.A.indptr, (const int32_t*)p.A.indices,
                        (const T*)p.A.values, (const IP*)p.B.indptr, (const int32_t*)p.B.indices,
                        (const T*)p.B.values, (const OUT*)cp, p.tj, (T*)p.tx, (T)1, p.row_cnt, p.seg,
-                       (int64_t)0, p.seg_len, (const int32_t*)p.spill, (const int32_t*)spill_counts(p, true));
+                       (int64_t)0, p.seg_len, (const int32_t*)p.spill, (const int32_t*)(p.scalars + 5));
     SPG_LAUNCHED(h);
     return SPG_STATUS_SUCCESS;
 }
@@ -772,6 +789,8 @@ spg_status_t spg_create(spg_handle_t* handle, int hip_device) {
     h->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     hipError_t e = hipSetDevice(dev);
     if (e == hipSuccess) e = hipHostMalloc((void**)&h->pinned, 16 * sizeof(int64_t), hipHostMallocDefault);
+    if (e == hipSuccess) e = hipMalloc((void**)&h->spill_ctr, 256);
+    if (e == hipSuccess) e = hipMemset(h->spill_ctr, 0, 256);
     if (e != hipSuccess) {
         delete h;
         return e == hipErrorOutOfMemory ? SPG_STATUS_ALLOC_FAILED : SPG_STATUS_HIP_ERROR;
@@ -787,6 +806,7 @@ spg_status_t spg_destroy(spg_handle_t h) {
         (void)hipFree(h->scratch);
     }
     if (h->pinned) (void)hipHostFree(h->pinned);
+    if (h->spill_ctr) (void)hipFree(h->spill_ctr);
     for (auto& q : h->pending) { (void)hipEventDestroy(q.a); (void)hipEventDestroy(q.b); }
     for (hipEvent_t e : h->pool) (void)hipEventDestroy(e);
     delete h;
@@ -888,7 +908,9 @@ spg_status_t spg_plan(spg_handle_t h, const spg_csr_t* A, const spg_csr_t* B, sp
     carve(*p, L);
     // control block: scalars + spill counters + scan status words, zeroed once per plan
     {
-        hipError_t e1 = hipMemsetAsync(p->ws, 0, L.row_cnt, h->stream);   // scalars + status
+        // (ALG1 on k_row zeroes what it uses itself)
+        hipError_t e1 = fused_alg1(*p) && p->use_row ? hipSuccess
+                                                     : hipMemsetAsync(p->ws, 0, L.row_cnt, h->stream);
         if (e1 != hipSuccess) { delete p; return hip_fail(h, e1); }
     }
     if (p->alg == SPG_ALG1 && !p->use_tile && !fused_alg1(*p)) {
@@ -926,10 +948,6 @@ spg_status_t spg_symbolic(spg_handle_t h, spg_plan_t p, void* C_indptr, spg_inde
         // the workspace's compact C -- no host sync in between.  A repeated call (the int64
         // retry after an int32 overflow, when the numeric pass wrote nothing) redoes the
         // scan and the numeric pass.
-        if (p->counts_ready) {
-            const int64_t tiles = scan_tiles(p->A.rows) + 1;
-            SPG_HIP(h, hipMemsetAsync(p->scan_status + tiles, 0, sizeof(unsigned long long) * tiles, h->stream));
-        }
         st = dispatch_value(p->A.value_type, [&](auto tag) {
             using T = decltype(tag);
             return i64 ? alg1_fused_typed<T, int64_t>(h, *p, C_indptr, C_indptr_type)
@@ -964,7 +982,7 @@ spg_status_t spg_symbolic(spg_handle_t h, spg_plan_t p, void* C_indptr, spg_inde
         p->fused_failed = true;
         p->symbolic_runs = 1;
         p->sym_spills = (int64_t)(uint32_t)(sc[5] & 0xffffffffu);   // the numeric pass relists them
-        SPG_HIP(h, hipMemsetAsync(spill_counts(*p, true), 0, sizeof(int32_t), h->stream));
+        SPG_HIP(h, hipMemsetAsync(p->scalars + 4, 0, 2 * sizeof(int64_t), h->stream));
         p->nnzC = sc[0];
         p->c_indptr = C_indptr;
         p->c_indptr_type = C_indptr_type;

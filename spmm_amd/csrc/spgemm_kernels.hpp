@@ -747,7 +747,9 @@ template <typename OUT>
 __global__ __launch_bounds__(BLOCK) void k_scan_lb(int64_t n, const int64_t* __restrict__ in,
                                                    OUT* __restrict__ out,
                                                    unsigned long long* __restrict__ status,
-                                                   int64_t* __restrict__ scalars) {
+                                                   int64_t* __restrict__ scalars,
+                                                   int32_t* __restrict__ move_cnt = nullptr,
+                                                   int64_t* __restrict__ move_dst = nullptr) {
     constexpr unsigned long long VMASK = (1ull << 62) - 1;
     __shared__ long long wsum[WPB];
     __shared__ long long prefix_s;
@@ -819,6 +821,10 @@ __global__ __launch_bounds__(BLOCK) void k_scan_lb(int64_t n, const int64_t* __r
         out[n] = (OUT)total;
         scalars[0] = total;
         scalars[1] = (sizeof(OUT) == 4 && total > 2147483647LL) ? 1 : 0;
+        if (move_cnt) {   // (ALG1 on k_row) hand the spill count over and re-arm the counter
+            *move_dst = *move_cnt;
+            *move_cnt = 0;
+        }
     }
 }
 

@@ -117,26 +117,34 @@ template <typename T, int NCMAX> struct RowOut {
     bool take;
 };
 
-// Lanes load their A entry, its value and its B row extent; the flattened product offset
-// of each entry goes to LDS.  Returns the row's product count P (wave-uniform).
-template <bool VALS, typename T, typename IP, typename Lds>
-__device__ __forceinline__ int row_front(Lds& S, int l, int64_t a0, int nA, const int32_t* __restrict__ Aj,
-                                         const T* __restrict__ Ax, const IP* __restrict__ Bp, int& cnt,
-                                         int& off) {
-    IP b0 = 0;
-    T av = (T)0;
-    cnt = 0;
+// A row's front: lane l loads its A entry, its value and its B row extent (registers only,
+// so the next row's front can be in flight while the current row is worked on).
+template <typename T, typename IP> struct RowFront {
+    IP b0;
+    int cnt;
+    T av;
+};
+template <bool VALS, typename T, typename IP>
+__device__ __forceinline__ RowFront<T, IP> row_front_load(int l, int64_t a0, int nA, const int32_t* __restrict__ Aj,
+                                                          const T* __restrict__ Ax, const IP* __restrict__ Bp) {
+    RowFront<T, IP> f{(IP)0, 0, (T)0};
     if (l < nA) {
         const int32_t k = Aj[a0 + l];
-        b0 = Bp[k];
-        cnt = (int)(Bp[k + 1] - b0);
-        if (VALS) av = Ax[a0 + l];
+        f.b0 = Bp[k];
+        f.cnt = (int)(Bp[k + 1] - f.b0);
+        if (VALS) f.av = Ax[a0 + l];
     }
-    const int incl = wave_incl_sum_dpp(cnt);
-    off = incl - cnt;
-    S.jb0[l] = b0;
+    return f;
+}
+// ... then the flattened product offset of each entry goes to LDS.  Returns the row's
+// product count P (wave-uniform).
+template <bool VALS, typename T, typename IP, typename Lds>
+__device__ __forceinline__ int row_front_commit(Lds& S, int l, const RowFront<T, IP>& f, int& off) {
+    const int incl = wave_incl_sum_dpp(f.cnt);
+    off = incl - f.cnt;
+    S.jb0[l] = f.b0;
     S.joff[l] = off;
-    if (VALS) S.ja[l] = av;
+    if (VALS) S.ja[l] = f.av;
     return readlane_i(incl, WAVE - 1);
 }
 
@@ -384,6 +392,10 @@ __device__ int row_count_only(Lds& S, int l, int64_t a0, int nA, const int32_t* 
 //     count pass listed them).  cap > 0 (ALG1, C's arrays hold `cap` entries): a row that
 //     would end past cap writes nothing (the host sees the total and redoes the product).
 enum { ROW_COUNT_ALL = 1, ROW_LISTED = 2 };
+#ifndef SPG_ROW_PAIR
+#define SPG_ROW_PAIR 1
+#endif
+constexpr int ROW_PAIR = SPG_ROW_PAIR;   // rows per wave (k_row)
 // register budget: 5 waves per SIMD (<= 96 VGPRs) for 4- and 8-byte values
 template <typename T, typename IP, typename OFF, int MODE, typename G>
 __global__ __launch_bounds__(G::WPB * WAVE, sizeof(T) <= 8 ? 5 : 3) void k_row(
@@ -392,49 +404,70 @@ __global__ __launch_bounds__(G::WPB * WAVE, sizeof(T) <= 8 ? 5 : 3) void k_row(
     const int32_t* __restrict__ Bj, const T* __restrict__ Bx, const OFF* __restrict__ Coff,
     int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha, int64_t* __restrict__ row_cnt,
     int32_t* __restrict__ spill, int32_t* __restrict__ spill_count, int flags, int64_t cap,
-    const int64_t* __restrict__ scan_scal) {
+    const int64_t* __restrict__ scan_scal, unsigned long long* __restrict__ zero_words = nullptr,
+    int64_t nzero = 0) {
     static_assert(MODE == ROW_SYM || MODE == ROW_NUM, "modes");
     constexpr bool VALS = MODE != ROW_SYM;
     __shared__ __attribute__((aligned(16))) RowLds<T, IP, G, VALS> lds[G::WPB];
+    // (ALG1 count pass) block 0 zeroes the next launch's scan status words: no memset
+    if (zero_words && blockIdx.x == 0)
+        for (int64_t i = threadIdx.x; i < nzero; i += G::WPB * WAVE) zero_words[i] = 0ull;
     const int l = lane_id();
     const int wv = uniform((int)(threadIdx.x >> 6));
     RowLds<T, IP, G, VALS>& S = lds[wv];
-    const int64_t it = (int64_t)blockIdx.x * G::WPB + wv;
-    if (it >= nrows) return;
-    const int64_t row = row0 + it;
     const bool count_all = MODE == ROW_SYM && (flags & ROW_COUNT_ALL);
+    // ROW_PAIR consecutive rows per wave: both rows' fronts (A entries, B row extents) are
+    // loaded before the first row is worked on, so the second row's dependent loads are
+    // in flight during the first row's gathers and LDS work
+    const int64_t it0 = ((int64_t)blockIdx.x * G::WPB + wv) * ROW_PAIR;
+    if (it0 >= nrows) return;
+    const int nr = (int)min((int64_t)ROW_PAIR, nrows - it0);
+    int64_t a0s[ROW_PAIR + 1];
+#pragma unroll
+    for (int q = 0; q <= ROW_PAIR; ++q) a0s[q] = q <= nr ? (int64_t)Ap[row0 + it0 + q] : 0;
+    RowFront<T, IP> fr[ROW_PAIR];
+#pragma unroll
+    for (int q = 0; q < ROW_PAIR; ++q) {
+        const int nAq = q < nr ? (int)(a0s[q + 1] - a0s[q]) : 0;
+        const bool f = nAq > 0 && nAq <= WAVE && ncols > 0;
+        fr[q] = row_front_load<VALS, T, IP>(l, a0s[q], f ? nAq : 0, Aj, Ax, Bp);
+    }
 
-    int64_t base = 0;
-    bool room = true;
-    if (MODE == ROW_NUM) {
-        base = (int64_t)Coff[row];
-        if (cap > 0) room = (int64_t)Coff[row + 1] <= cap;
-        // (ALG1) an int32 row pointer that overflowed (scan scalars[1]) is not an offset
-        if (scan_scal && scan_scal[1]) room = false;
-    }
-    const int64_t a0 = Ap[row];
-    const int nA = (int)(Ap[row + 1] - a0);
-    int cnt = 0, off = 0, P = 0;
-    bool fits = nA > 0 && nA <= WAVE && ncols > 0;
-    if (fits) {
-        P = row_front<VALS, T, IP>(S, l, a0, nA, Aj, Ax, Bp, cnt, off);
-        fits = P <= G::PREG;
-    }
-    const bool empty = nA <= 0 || ncols <= 0 || (fits && P == 0);
-    bool take = false;
-    int nnz = 0;
-    if (fits && P > 0) {
-        row_dispatch<VALS, T, IP, G>(S, l, cnt, off, P, Bj, Bx, [&](const auto& o) {
-            take = o.take;
-            nnz = o.nnz;
-            if (take && MODE == ROW_NUM && room) row_write(o, Cj + base, Cx + base, alpha);
-        });
-    }
-    if (!empty && !take) {
-        if (count_all && !(fits && P > 0)) nnz = row_count_only<IP>(S, l, a0, nA, Aj, Bp, Bj);
-        if (l == 0 && !(flags & ROW_LISTED)) spill[atomicAdd(spill_count, 1)] = (int32_t)row;
-    }
-    if (MODE == ROW_SYM && l == 0 && (take || empty || count_all)) row_cnt[row] = take || count_all ? nnz : 0;
+    auto do_row = [&](int64_t row, int64_t a0, int nA, const RowFront<T, IP>& f) {
+        int64_t base = 0;
+        bool room = true;
+        if (MODE == ROW_NUM) {
+            base = (int64_t)Coff[row];
+            if (cap > 0) room = (int64_t)Coff[row + 1] <= cap;
+            // (ALG1) an int32 row pointer that overflowed (scan scalars[1]) is not an offset
+            if (scan_scal && scan_scal[1]) room = false;
+        }
+        int off = 0, P = 0;
+        bool fits = nA > 0 && nA <= WAVE && ncols > 0;
+        if (fits) {
+            P = row_front_commit<VALS, T, IP>(S, l, f, off);
+            fits = P <= G::PREG;
+        }
+        const bool empty = nA <= 0 || ncols <= 0 || (fits && P == 0);
+        bool take = false;
+        int nnz = 0;
+        if (fits && P > 0) {
+            row_dispatch<VALS, T, IP, G>(S, l, f.cnt, off, P, Bj, Bx, [&](const auto& o) {
+                take = o.take;
+                nnz = o.nnz;
+                if (take && MODE == ROW_NUM && room) row_write(o, Cj + base, Cx + base, alpha);
+            });
+        }
+        if (!empty && !take) {
+            if (count_all && !(fits && P > 0)) nnz = row_count_only<IP>(S, l, a0, nA, Aj, Bp, Bj);
+            if (l == 0 && !(flags & ROW_LISTED)) spill[atomicAdd(spill_count, 1)] = (int32_t)row;
+        }
+        if (MODE == ROW_SYM && l == 0 && (take || empty || count_all)) row_cnt[row] = take || count_all ? nnz : 0;
+        wsync();   // the next row reuses this wave's LDS
+    };
+#pragma unroll
+    for (int q = 0; q < ROW_PAIR; ++q)
+        if (q < nr) do_row(row0 + it0 + q, a0s[q], (int)(a0s[q + 1] - a0s[q]), fr[q]);
 }
 
 }  // namespace spg
