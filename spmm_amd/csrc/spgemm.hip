@@ -255,13 +255,14 @@ spg_status_t ensure_scratch(spg_handle_t h, size_t bytes) {
 template <typename OUT>
 spg_status_t launch_scan(spg_handle_t h, int64_t n, const int64_t* in, OUT* out,
                          unsigned long long* status, int64_t* scal, bool zero_status,
-                         int32_t* move_cnt = nullptr, int64_t* move_dst = nullptr) {
+                         int32_t* move_cnt = nullptr, int64_t* move_dst = nullptr,
+                         int64_t* host_mirror = nullptr) {
     const int64_t tiles = scan_tiles(n);
     if (zero_status)
         SPG_HIP(h, hipMemsetAsync(status, 0, sizeof(unsigned long long) * (size_t)(tiles + 1), h->stream));
     PhaseTimer pt(h, SPG_PHASE_SCAN);
     hipLaunchKernelGGL(k_scan_lb<OUT>, dim3((unsigned)tiles), dim3(BLOCK), 0, h->stream, n, in, out,
-                       status, scal, move_cnt, move_dst);
+                       status, scal, move_cnt, move_dst, host_mirror);
     SPG_LAUNCHED(h);
     return SPG_STATUS_SUCCESS;
 }
@@ -329,9 +330,12 @@ spg_status_t scratch_for_products(spg_handle_t h, int64_t rows, ScratchView& v) 
     return SPG_STATUS_SUCCESS;
 }
 
+// Waits for the handle's stream (polling hipStreamQuery measured slower on the box).
+hipError_t stream_wait(spg_handle_t h) { return hipStreamSynchronize(h->stream); }
+
 spg_status_t read_scalars(spg_handle_t h, const int64_t* dev, int n, int64_t* out) {
     SPG_HIP(h, hipMemcpyAsync(h->pinned, dev, sizeof(int64_t) * n, hipMemcpyDeviceToHost, h->stream));
-    SPG_HIP(h, hipStreamSynchronize(h->stream));
+    SPG_HIP(h, stream_wait(h));
     for (int i = 0; i < n; ++i) out[i] = h->pinned[i];
     return SPG_STATUS_SUCCESS;
 }
@@ -618,7 +622,7 @@ spg_status_t alg1_fused_run(spg_handle_t h, spg_plan_s& p, void* cp) {
                                (int)ROW_COUNT_ALL, (int64_t)0, (const int64_t*)nullptr, status, nstatus);
             SPG_LAUNCHED(h);
             spg_status_t st = launch_scan<OUT>(h, p.A.rows, (const int64_t*)p.row_cnt, (OUT*)cp, status,
-                                               p.scalars, false, h->spill_ctr, p.scalars + 5);
+                                               p.scalars, false, h->spill_ctr, p.scalars + 5, h->pinned);
             if (st) return st;
             h->spill_ctr_dirty = false;
         } else {   // repeated call: the first scan already moved the spill count
@@ -954,9 +958,16 @@ spg_status_t spg_symbolic(spg_handle_t h, spg_plan_t p, void* C_indptr, spg_inde
                        : alg1_fused_typed<T, int32_t>(h, *p, C_indptr, C_indptr_type);
         });
         if (st) return st;
-        p->counts_ready = true;
         int64_t sc[6];
-        if ((st = read_scalars(h, p->scalars, 6, sc))) return st;
+        if (!p->counts_ready) {
+            // the scan mirrored total / overflow / spills into the pinned buffer: wait for the
+            // stream (no device->host copy)
+            SPG_HIP(h, stream_wait(h));
+            for (int i = 0; i < 6; ++i) sc[i] = ((volatile int64_t*)h->pinned)[i];
+        } else if ((st = read_scalars(h, p->scalars, 6, sc))) {
+            return st;
+        }
+        p->counts_ready = true;
         if (sc[1]) return SPG_STATUS_OVERFLOW;   // int32 row pointer: retry with int64
         if (sc[0] <= p->cap) {
             p->alg1_fused = true;

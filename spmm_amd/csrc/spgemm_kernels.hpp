@@ -749,7 +749,8 @@ __global__ __launch_bounds__(BLOCK) void k_scan_lb(int64_t n, const int64_t* __r
                                                    unsigned long long* __restrict__ status,
                                                    int64_t* __restrict__ scalars,
                                                    int32_t* __restrict__ move_cnt = nullptr,
-                                                   int64_t* __restrict__ move_dst = nullptr) {
+                                                   int64_t* __restrict__ move_dst = nullptr,
+                                                   int64_t* __restrict__ host_mirror = nullptr) {
     constexpr unsigned long long VMASK = (1ull << 62) - 1;
     __shared__ long long wsum[WPB];
     __shared__ long long prefix_s;
@@ -821,9 +822,16 @@ __global__ __launch_bounds__(BLOCK) void k_scan_lb(int64_t n, const int64_t* __r
         out[n] = (OUT)total;
         scalars[0] = total;
         scalars[1] = (sizeof(OUT) == 4 && total > 2147483647LL) ? 1 : 0;
+        int64_t moved = 0;
         if (move_cnt) {   // (ALG1 on k_row) hand the spill count over and re-arm the counter
-            *move_dst = *move_cnt;
+            moved = *move_cnt;
+            *move_dst = moved;
             *move_cnt = 0;
+        }
+        if (host_mirror) {   // total, overflow, spills straight to pinned host memory
+            __hip_atomic_store(&host_mirror[0], (int64_t)total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&host_mirror[1], (int64_t)scalars[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&host_mirror[5], moved, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
 }
