@@ -11,13 +11,20 @@ SRC      := spmm_amd/csrc/spgemm.hip
 HDRS     := include/spgemm.h $(wildcard spmm_amd/csrc/*.hpp)
 DRIVERS  := drivers/bin/spgemm_from_txt_alg1 drivers/bin/spgemm_from_txt_alg2 drivers/bin/spgemm_from_txt_alg3
 
-all: lib drivers oracle
+FASTPATH := spmm_amd/lib/fastpath/spmm_fastpath.so
+
+all: lib drivers oracle fastpath
 lib: $(LIB)
 drivers: $(DRIVERS)
+fastpath: $(FASTPATH)
+
+# torch C++ extension of the Python shim (links the library above; no device code)
+$(FASTPATH): spmm_amd/csrc/fastpath.cpp include/spgemm.h spmm_amd/build_fastpath.py $(LIB)
+	python3 spmm_amd/build_fastpath.py
 
 $(LIB): $(SRC) $(HDRS)
 	@mkdir -p $(dir $@)
-	$(HIPCC) $(HIPFLAGS) -shared -Iinclude -Ispmm_amd/csrc $(SRC) -o $@
+	$(HIPCC) $(HIPFLAGS) -shared -Wl,-soname,libmi355_spgemm.so -Iinclude -Ispmm_amd/csrc $(SRC) -o $@
 
 # the three reference driver names, one source; ALG fixed at compile time
 drivers/bin/spgemm_from_txt_alg%: drivers/spgemm_from_txt.cpp include/spgemm.h $(LIB)
@@ -31,6 +38,7 @@ oracle:
 
 clean:
 	rm -f $(LIB) $(DRIVERS)
+	rm -rf spmm_amd/lib/fastpath
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all lib drivers oracle clean
+.PHONY: all lib drivers oracle fastpath clean

@@ -25,7 +25,7 @@ from dataclasses import dataclass
 import numpy as np
 import torch
 
-from . import _lib
+from . import _fastpath, _lib
 from ._lib import SpgCsr, SpgError, check
 from .sparse import csr_matrix
 
@@ -142,9 +142,21 @@ def spgemm(a, b, alpha=1, alg=0, chunk_fraction=0.2, verbose=False):
 
     dev = a.device
     h = _handle_for(a)
+    cf = float(chunk_fraction)
+    fp = _fastpath.get()
+    if fp is not None:   # the same sequence in one native call (csrc/fastpath.cpp)
+        al = complex(alpha)
+        st, data, indices, indptr, wsb, peak = fp.spgemm(
+            h.ptr.value, m, a.shape[1], n, a.indptr, a.indices, a.data, b.indptr, b.indices, b.data,
+            int(algo), cf, al.real, al.imag)
+        check(st, "spg_spgemm_ws")
+        if verbose:
+            print("USING ALG", alg, "workspace GB =", wsb / (1024 ** 3))
+        last_stats.alg, last_stats.workspace_bytes = int(algo), int(wsb)
+        last_stats.peak_bytes, last_stats.nnz = int(peak), int(indices.numel())
+        return csr_matrix._from_parts(data, indices, indptr, (m, n), canonical=True)
     lib = h.lib
     va, vb = _csr_view(a), _csr_view(b)
-    cf = float(chunk_fraction)
     ws_bytes = ctypes.c_size_t(0)
     check(lib.spg_plan(h.ptr, ctypes.byref(va), ctypes.byref(vb), algo, cf,
                        ctypes.byref(ws_bytes), None, None), "spg_plan")

@@ -128,3 +128,14 @@ def test_harness_scripts_compile():
             if f.endswith(".sh"):
                 subprocess.run(["bash", "-n", os.path.join(dp, f)], check=True)
     assert n >= 12
+
+
+def test_fastpath_extension_loads():
+    """The shim's native path (csrc/fastpath.cpp) is prebuilt in-tree and binds to the
+    already-loaded engine (soname libmi355_spgemm.so); no compute without a GPU."""
+    import os
+    from spmm_amd import _fastpath
+    if not os.path.exists(_fastpath.PATH):
+        pytest.skip("fast path not built (make fastpath)")
+    fp = _fastpath.get()
+    assert fp is not None and hasattr(fp, "spgemm")
