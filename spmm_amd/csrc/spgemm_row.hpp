@@ -298,8 +298,8 @@ __device__ __forceinline__ void row_pass(Lds& S, int l, int cnt, int off, int P,
     }
 }
 
-// P in [1, PREG]: the register path with the smallest chunk count that holds P (even
-// counts), then `then(o)` on its result -- inside each case, so the result of one case
+// P in [1, PREG]: the register path with the smallest chunk count that holds P, then
+// `then(o)` on its result -- inside each case, so the result of one case
 // never meets another's at a join (it would otherwise occupy registers for all five).
 template <bool VALS, typename T, typename IP, typename G, typename Lds, typename F>
 __device__ __forceinline__ void row_dispatch(Lds& S, int l, int cnt, int off, int P, const int32_t* __restrict__ Bj,
@@ -311,32 +311,43 @@ __device__ __forceinline__ void row_dispatch(Lds& S, int l, int cnt, int off, in
         row_pass<NC, VALS, T, IP, G>(S, l, cnt, off, P, Bj, Bx, o);
         then(o);
     };
-    switch (((P + WAVE - 1) / WAVE + 1) >> 1) {
-        case 1: run(IntC<2>{}); break;
-        case 2: run(IntC<4>{}); break;
-        case 3: run(IntC<6>{}); break;
-        case 4: run(IntC<8>{}); break;
+    switch ((P + WAVE - 1) / WAVE) {   // exact chunk counts where rows are common
+        case 1:
+        case 2: run(IntC<2>{}); break;
+        case 3: run(IntC<3>{}); break;
+        case 4: run(IntC<4>{}); break;
+        case 5: run(IntC<5>{}); break;
+        case 6: run(IntC<6>{}); break;
+        case 7: run(IntC<7>{}); break;
+        case 8: run(IntC<8>{}); break;
         default: run(IntC<10>{}); break;
     }
 }
 
 // Unflagged products straight from registers, then the list leaders.
-template <typename T, int NCMAX>
-__device__ __forceinline__ void row_write(const RowOut<T, NCMAX>& o, int32_t* __restrict__ crow,
-                                          T* __restrict__ xrow, T alpha) {
+template <bool UNIT, typename T, int NCMAX>
+__device__ __forceinline__ void row_write_a(const RowOut<T, NCMAX>& o, int32_t* __restrict__ crow,
+                                            T* __restrict__ xrow, T alpha) {
 #pragma unroll
     for (int r = 0; r < NCMAX; ++r) {
         const int c = o.cp[r];
         if (c >= 0 && !(c & CP_FLAG)) {
             const int p = (c >> CP_POS) & 0x3fff;
             crow[p] = c & 0x3fff;
-            xrow[p] = scale(alpha, add_rn((T)0, o.prd[r]));
+            const T v = add_rn((T)0, o.prd[r]);
+            xrow[p] = UNIT ? v : mul_rn(alpha, v);
         }
     }
     if (o.lcol >= 0) {
         crow[o.lpos] = o.lcol;
-        xrow[o.lpos] = scale(alpha, o.lsum);
+        xrow[o.lpos] = UNIT ? o.lsum : mul_rn(alpha, o.lsum);
     }
+}
+template <typename T, int NCMAX>
+__device__ __forceinline__ void row_write(const RowOut<T, NCMAX>& o, int32_t* __restrict__ crow,
+                                          T* __restrict__ xrow, T alpha) {
+    if (alpha == (T)1) row_write_a<true>(o, crow, xrow, alpha);   // (uniform branch)
+    else row_write_a<false>(o, crow, xrow, alpha);
 }
 
 // Structural nnz of any row with <= 16384 columns: 64 A entries at a time, chunk by chunk
