@@ -47,13 +47,23 @@ template <int R_, int LCAP_, int WPB_> struct RowCfg {
 };
 using RowSmall = RowCfg<10, 64, 4>;
 
+// One record per A entry, read with one wide LDS access per chunk (16 B for int32 row
+// pointers and f64 values).
+template <typename T, typename IP, bool VALS> struct alignas(VALS ? (sizeof(IP) + 4 + sizeof(T) >= 16 ? 16 : 8) : 8) JRec {
+    IP jb0;         // B row start
+    int32_t joff;   // first flattened product
+    T ja;           // A value (VALS)
+};
+template <typename T, typename IP> struct alignas(8) JRec<T, IP, false> {
+    IP jb0;
+    int32_t joff;
+};
+
 template <typename T, typename IP, typename G, bool VALS, int SCAP = 0> struct RowLds {
     uint32_t bits[G::NW];
     uint16_t wpre[G::NW];          // exclusive popcount prefix | 0x8000 for flagged words
     uint32_t dupw[G::NW / 32];     // one bit per bitmap word: a column of it was hit twice
-    IP jb0[WAVE];                  // B row start of each A entry
-    int32_t joff[WAVE];            // first flattened product of each A entry
-    T ja[VALS ? WAVE : 1];         // A values
+    JRec<T, IP, VALS> jr[WAVE];    // per A entry: B row start, first product, value
     union {                        // phases of one row that never overlap:
         int8_t mk[G::MKB];         //   lane -> A-entry markers of every chunk (pass 1)
         struct {                   //   flagged-word products in product order (fix-up)
@@ -142,9 +152,8 @@ template <bool VALS, typename T, typename IP, typename Lds>
 __device__ __forceinline__ int row_front_commit(Lds& S, int l, const RowFront<T, IP>& f, int& off) {
     const int incl = wave_incl_sum_dpp(f.cnt);
     off = incl - f.cnt;
-    S.jb0[l] = f.b0;
-    S.joff[l] = off;
-    if (VALS) S.ja[l] = f.av;
+    if constexpr (VALS) S.jr[l] = JRec<T, IP, VALS>{f.b0, off, f.av};
+    else S.jr[l] = JRec<T, IP, VALS>{f.b0, off};
     return readlane_i(incl, WAVE - 1);
 }
 
@@ -179,10 +188,19 @@ __device__ __forceinline__ void row_pass(Lds& S, int l, int cnt, int off, int P,
         }
     }
     IP idx[NC];
+    T av[NC];
 #pragma unroll
     for (int r = 0; r < NC; ++r) {
         const int t = r * WAVE + l;
-        idx[r] = t < P ? S.jb0[src[r]] + (IP)(t - S.joff[src[r]]) : (IP)0;
+        JRec<T, IP, VALS> j;
+        if constexpr (sizeof(j) == 16) {   // one ds_read_b128
+            const uint4 q = *reinterpret_cast<const uint4*>(&S.jr[src[r]]);
+            __builtin_memcpy(&j, &q, 16);
+        } else {
+            j = S.jr[src[r]];
+        }
+        idx[r] = t < P ? j.jb0 + (IP)(t - j.joff) : (IP)0;
+        if constexpr (VALS) av[r] = j.ja;
     }
     // every product of the row in flight at once
     int col[NC];
@@ -193,7 +211,7 @@ __device__ __forceinline__ void row_pass(Lds& S, int l, int cnt, int off, int P,
 #pragma unroll
         for (int r = 0; r < NC; ++r) bx[r] = ld_idx(Bx, idx[r]);
 #pragma unroll
-        for (int r = 0; r < NC; ++r) o.prd[r] = mul_rn(S.ja[src[r]], bx[r]);
+        for (int r = 0; r < NC; ++r) o.prd[r] = mul_rn(av[r], bx[r]);
     }
 #pragma unroll
     for (int r = 0; r < NC; ++r)
@@ -370,8 +388,8 @@ __device__ int row_count_only(Lds& S, int l, int64_t a0, int nA, const int32_t* 
         const int bincl = wave_incl_sum(bc);
         const int boff = bincl - bc;
         const int bP = readlane_i(bincl, WAVE - 1);
-        S.jb0[l] = bb;
-        S.joff[l] = boff;
+        S.jr[l].jb0 = bb;
+        S.jr[l].joff = boff;
         int carry = -1;
         for (int c0 = 0; c0 < bP; c0 += WAVE) {
             S.marker[l] = -1;
@@ -381,7 +399,7 @@ __device__ int row_count_only(Lds& S, int l, int64_t a0, int nA, const int32_t* 
             const int src = max(wave_incl_max_dpp((int)S.marker[l]), carry);
             carry = readlane_i(src, WAVE - 1);
             const int t = c0 + l;
-            if (t < bP) set_bit(S.bits, Bj[S.jb0[src] + (IP)(t - S.joff[src])]);
+            if (t < bP) set_bit(S.bits, Bj[S.jr[src].jb0 + (IP)(t - S.jr[src].joff)]);
         }
         wsync();
     }
