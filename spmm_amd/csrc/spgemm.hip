@@ -22,12 +22,14 @@
 
 using namespace spg;
 
+constexpr int PINNED_WORDS = 16 + 1024;   // host-pinned scalars: 16 + per-chunk spill counts
+
 struct spg_handle_s {
     int device = 0;
     int cus = 256;                  // compute units (persistent grids)
     hipStream_t stream = nullptr;
     int last_hip = 0;
-    int64_t* pinned = nullptr;      // 8 host-pinned int64 for device->host scalars
+    int64_t* pinned = nullptr;      // PINNED_WORDS host-pinned int64 for device->host scalars
     int32_t* spill_ctr = nullptr;   // ALG1 on k_row: spill counter, re-armed by the scan kernel
     bool spill_ctr_dirty = false;   // a count pass ran without its scan (re-zero first)
     void* scratch = nullptr;        // internal device scratch (plan-time analysis)
@@ -81,6 +83,12 @@ struct spg_plan_s {
     bool fused_failed = false;      // the single pass met a row it cannot take
     bool scaled_in_place = false;   // spg_numeric scaled the workspace result by alpha
     int64_t sym_spills = -1;        // rows the symbolic short-row pass spilled (-1 unknown)
+    // ALG2/ALG3 on k_row: the count pass counts spilled rows itself and lists each chunk's
+    // spills at p.spill + (chunk's first row), counted in cspill[c] (int32 in an int64 slot
+    // after the 16 scalars); the numeric general kernel runs only for chunks with spills
+    int64_t nspc = 0;
+    int64_t* cspill = nullptr;
+    std::vector<int64_t> chunk_spills;
     int64_t cap = 0;                // ALG1 single pass: entries tj/tx hold (an estimate)
     uint2* tidx = nullptr;          // B column-tile index, B.rows * G (start, end) pairs
     void* brec = nullptr;           // B packed as (column, value) records (numeric tile pass)
@@ -334,6 +342,7 @@ spg_status_t scratch_for_products(spg_handle_t h, int64_t rows, ScratchView& v) 
 hipError_t stream_wait(spg_handle_t h) { return hipStreamSynchronize(h->stream); }
 
 spg_status_t read_scalars(spg_handle_t h, const int64_t* dev, int n, int64_t* out) {
+    if (n > PINNED_WORDS) return SPG_STATUS_INTERNAL_ERROR;
     SPG_HIP(h, hipMemcpyAsync(h->pinned, dev, sizeof(int64_t) * n, hipMemcpyDeviceToHost, h->stream));
     SPG_HIP(h, stream_wait(h));
     for (int i = 0; i < n; ++i) out[i] = h->pinned[i];
@@ -364,7 +373,7 @@ inline unsigned long long* item_scan_status(const spg_plan_s& p) {
 Layout make_layout(const spg_plan_s& p) {
     Layout L;
     size_t off = 0;
-    L.scalars = off; off = align_up(off + 16 * sizeof(int64_t));
+    L.scalars = off; off = align_up(off + (16 + (size_t)p.nspc) * sizeof(int64_t));
     L.status = off;  off = align_up(off + sizeof(unsigned long long) * status_words(p));
     L.row_cnt = off; off = align_up(off + sizeof(int64_t) * (size_t)(p.A.rows + 1));
     L.seg = off;     off = align_up(off + sizeof(uint32_t) * 2 * (size_t)std::max<int64_t>(p.seg_len, 1));
@@ -388,6 +397,7 @@ Layout make_layout(const spg_plan_s& p) {
 
 void carve(spg_plan_s& p, const Layout& L) {
     p.scalars = (int64_t*)(p.ws + L.scalars);
+    p.cspill = p.nspc > 0 ? p.scalars + 16 : nullptr;
     p.row_cnt = (int64_t*)(p.ws + L.row_cnt);
     p.seg = (uint32_t*)(p.ws + L.seg);
     p.spill = (int32_t*)(p.ws + L.spill);
@@ -462,7 +472,7 @@ inline int32_t* spill_counts(spg_plan_s& p, bool numeric) {
 }
 
 template <typename IP>
-spg_status_t run_symbolic_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_t r1, int64_t nz0) {
+spg_status_t run_symbolic_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_t r1, int64_t nz0, int chunk = 0) {
     const int64_t n = r1 - r0;
     if (n <= 0) return SPG_STATUS_SUCCESS;
     const IP* Ap = (const IP*)p.A.indptr;
@@ -482,6 +492,15 @@ spg_status_t run_symbolic_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_
         hipLaunchKernelGGL(k_tile_sym<IP>, dim3(tile_grid(n * ((p.G + R - 1) / R))), dim3(TILE_WPB * WAVE), 0,
                            h->stream, r0, n, p.tws, p.G, p.twss, Ap, Aj, Bp, Bj, (const uint2*)p.tidx,
                            p.bitmap, p.item_cnt);
+    } else if (p.use_short && p.nspc > 0) {
+        // k_row counts every row (spills by the chunked loop) and lists this chunk's spills
+        PhaseTimer pt(h, SPG_PHASE_SYMBOLIC);
+        hipLaunchKernelGGL((k_row<double, IP, int64_t, ROW_SYM, RowSmall>),
+                           dim3((unsigned)grid_for(n, RowSmall::WPB * ROW_PAIR)), dim3(RowSmall::WPB * WAVE), 0,
+                           h->stream, r0, n, p.B.cols, Ap, Aj, (const double*)nullptr, Bp, Bj,
+                           (const double*)nullptr, (const int64_t*)nullptr, (int32_t*)nullptr, (double*)nullptr,
+                           1.0, p.row_cnt, p.spill + r0, (int32_t*)(p.cspill + chunk), (int)ROW_COUNT_ALL,
+                           (int64_t)0, (const int64_t*)nullptr);
     } else if (p.use_short) {
         int32_t* cnt = spill_counts(p, false);
         int32_t* l1 = p.spill;
@@ -520,7 +539,7 @@ spg_status_t run_symbolic_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_
 
 template <typename T, typename IP, typename OFF, bool UB>
 spg_status_t run_numeric_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_t r1, int64_t nz0,
-                              const OFF* off, int32_t* cj, T* cx, T alpha) {
+                              const OFF* off, int32_t* cj, T* cx, T alpha, int chunk = 0) {
     const int64_t n = r1 - r0;
     if (n <= 0) return SPG_STATUS_SUCCESS;
     const IP* Ap = (const IP*)p.A.indptr;
@@ -542,6 +561,22 @@ spg_status_t run_numeric_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_t
         hipLaunchKernelGGL((k_tile<T, IP>), dim3(tile_grid(n * p.G)), dim3(TILE_WPB * WAVE), 0, h->stream, r0,
                            n, p.tws, p.G, Ap, Aj, Ax, Bp, (const BRec<T>*)p.brec, (const uint2*)p.tidx,
                            (const uint32_t*)p.bitmap, (const int64_t*)p.item_cnt, cj, cx, alpha);
+    } else if (p.use_short && p.nspc > 0 && !UB) {
+        {
+            PhaseTimer pt(h, SPG_PHASE_NUMERIC);
+            hipLaunchKernelGGL((k_row<T, IP, OFF, ROW_NUM, RowSmall>), dim3((unsigned)grid_for(n, RowSmall::WPB * ROW_PAIR)),
+                               dim3(RowSmall::WPB * WAVE), 0, h->stream, r0, n, p.B.cols, Ap, Aj, Ax, Bp, Bj, Bx,
+                               off, cj, cx, alpha, p.row_cnt, p.spill + r0, (int32_t*)(p.cspill + chunk),
+                               (int)ROW_LISTED, (int64_t)0, (const int64_t*)nullptr);
+            SPG_LAUNCHED(h);
+        }
+        // the general kernel only for a chunk whose count pass listed rows
+        if ((size_t)chunk < p.chunk_spills.size() && p.chunk_spills[(size_t)chunk] == 0) return SPG_STATUS_SUCCESS;
+        PhaseTimer ps(h, SPG_PHASE_SPILL);
+        hipLaunchKernelGGL((k_numeric<T, IP, OFF, UB>), dim3(p.list_grid), dim3(BLOCK), 0, h->stream,
+                           r0, n, p.B.cols, Ap, Aj, Ax, Bp, Bj, Bx, off, cj, cx, alpha, p.row_cnt,
+                           p.seg, nz0, p.seg_len, (const int32_t*)(p.spill + r0),
+                           (const int32_t*)(p.cspill + chunk));
     } else if (p.use_short) {
         int32_t* cnt = spill_counts(p, true);
         int32_t* l1 = p.spill;
@@ -676,9 +711,9 @@ spg_status_t symbolic_typed(spg_handle_t h, spg_plan_s& p) {
     spg_status_t st;
     if (p.alg == SPG_ALG3) {
         for (size_t c = 0; c + 1 < p.chunk_rows.size(); ++c) {
-            if (c > 0 && p.use_short)
+            if (c > 0 && p.use_short && p.nspc == 0)
                 SPG_HIP(h, hipMemsetAsync(spill_counts(p, false), 0, 2 * sizeof(int32_t), h->stream));
-            if ((st = run_symbolic_rows<IP>(h, p, p.chunk_rows[c], p.chunk_rows[c + 1], p.chunk_nz[c])))
+            if ((st = run_symbolic_rows<IP>(h, p, p.chunk_rows[c], p.chunk_rows[c + 1], p.chunk_nz[c], (int)c)))
                 return st;
         }
         return SPG_STATUS_SUCCESS;
@@ -725,11 +760,11 @@ spg_status_t numeric_typed(spg_handle_t h, spg_plan_s& p, const spg_csr_t& C, T 
     spg_status_t st;
     if (p.alg == SPG_ALG3) {
         for (size_t c = 0; c + 1 < p.chunk_rows.size(); ++c) {
-            if (c > 0 && p.use_short)
+            if (c > 0 && p.use_short && p.nspc == 0)
                 SPG_HIP(h, hipMemsetAsync(spill_counts(p, true), 0, 2 * sizeof(int32_t), h->stream));
             if ((st = run_numeric_rows<T, IP, IPC, false>(h, p, p.chunk_rows[c], p.chunk_rows[c + 1],
                                                           p.chunk_nz[c], cp, (int32_t*)C.indices,
-                                                          (T*)C.values, alpha)))
+                                                          (T*)C.values, alpha, (int)c)))
                 return st;
         }
         return SPG_STATUS_SUCCESS;
@@ -792,7 +827,7 @@ spg_status_t spg_create(spg_handle_t* handle, int hip_device) {
     h->device = dev;
     h->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     hipError_t e = hipSetDevice(dev);
-    if (e == hipSuccess) e = hipHostMalloc((void**)&h->pinned, 16 * sizeof(int64_t), hipHostMallocDefault);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&h->pinned, PINNED_WORDS * sizeof(int64_t), hipHostMallocDefault);
     if (e == hipSuccess) e = hipMalloc((void**)&h->spill_ctr, 256);
     if (e == hipSuccess) e = hipMemset(h->spill_ctr, 0, 256);
     if (e != hipSuccess) {
@@ -888,6 +923,10 @@ spg_status_t spg_plan(spg_handle_t h, const spg_csr_t* A, const spg_csr_t* B, sp
         }
     }
     if (tmp.use_tile) tmp.seg_len = 1;   // no cursor scratch on the tile path
+    if (tmp.use_short && tmp.use_row && (tmp.alg == SPG_ALG2 || tmp.alg == SPG_ALG3)) {
+        const int64_t nch = tmp.alg == SPG_ALG3 ? (int64_t)tmp.chunk_rows.size() - 1 : 1;
+        if (nch >= 1 && nch <= PINNED_WORDS - 16) tmp.nspc = nch;
+    }
     if (!workspace) {
         h->q_valid = true;
         h->q_A = *A;
@@ -1078,7 +1117,15 @@ spg_status_t spg_symbolic(spg_handle_t h, spg_plan_t p, void* C_indptr, spg_inde
                                         : run_scan<int32_t>(h, *p, C_indptr);
     if (st) return st;
     int64_t sc[5];
-    if ((st = read_scalars(h, p->scalars, 5, sc))) return st;
+    if (p->nspc > 0 && !p->counts_ready) {   // scalars + every chunk's spill count, one read
+        std::vector<int64_t> all((size_t)(16 + p->nspc));
+        if ((st = read_scalars(h, p->scalars, (int)all.size(), all.data()))) return st;
+        for (int i = 0; i < 5; ++i) sc[i] = all[(size_t)i];
+        p->chunk_spills.assign(all.begin() + 16, all.end());
+        for (auto& v : p->chunk_spills) v &= 0xffffffffLL;
+    } else if ((st = read_scalars(h, p->scalars, 5, sc))) {
+        return st;
+    }
     // the short-row kernel spills the same rows in both passes: none in the symbolic pass
     // (one launch over all rows) means the numeric spill launch can be skipped
     if (p->use_short && (p->alg == SPG_ALG2 || fused_alg1(*p))) p->sym_spills = (int64_t)(uint32_t)(sc[4] & 0xffffffffu);
