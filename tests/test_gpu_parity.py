@@ -447,3 +447,72 @@ def test_upstream_testspgemm_complex():
                 assert c.nnz > 0
                 continue
             np.testing.assert_array_almost_equal(c.toarray(), (0.5 * a.dot(b)).toarray())
+
+
+def test_shim_paths_agree(monkeypatch):
+    """The native shim (csrc/fastpath.cpp) and the ctypes shim run the same C ABI: bit-equal
+    results, the same stats, for every algorithm, alpha != 1 and fp32."""
+    from spmm_amd import _fastpath
+    rng = np.random.default_rng(61)
+    for dt in (np.float64, np.float32):
+        A = sp.random(3000, 2500, density=0.006, format="csr", random_state=rng, dtype=dt)
+        B = sp.random(2500, 4000, density=0.005, format="csr", random_state=rng, dtype=dt)
+        A.sort_indices(); B.sort_indices()
+        ref = oracle.spgemm(A, B, alpha=-1.25, keep_zeros=True, sort=True)
+        for alg in (1, 2, 3):
+            fast = _gpu(A, B, alg=alg, alpha=-1.25, cf=0.3)
+            _assert_same(fast, ref)
+            monkeypatch.setattr(_fastpath, "_mod", None)
+            monkeypatch.setattr(_fastpath, "_tried", True)   # ctypes path only
+            slow = _gpu(A, B, alg=alg, alpha=-1.25, cf=0.3)
+            monkeypatch.undo()
+            _assert_same(slow, ref)
+
+
+def test_spgemm_ws_abi():
+    """spg_spgemm_ws through ctypes: ALG1 returns C in the workspace (complete, scaled), ALG2
+    returns the live plan for the caller's spg_numeric; both bit-exact."""
+    import ctypes
+    from spmm_amd import _lib, gen
+    from spmm_amd._lib import SpgCsr
+    from spmm_amd.sparse import csr_matrix
+    Ah, Bh = gen.scipy_pair(4096, 1.5e-3, seed=71)
+    ref = oracle.spgemm(Ah, Bh, alpha=0.5, keep_zeros=True, sort=True)
+    A, B = csr_matrix(Ah, device=_dev()), csr_matrix(Bh, device=_dev())
+    h = _lib.get_handle(0)
+    h.set_stream(torch.cuda.current_stream().cuda_stream)
+    lib = h.lib
+
+    def view(M):
+        return SpgCsr(M.shape[0], M.shape[1], M.nnz, M.indptr.data_ptr(), M.indices.data_ptr(),
+                      M.data.data_ptr(), _lib.SPG_INDEX_32I, _lib.SPG_R_64F)
+
+    va, vb = view(A), view(B)
+    al = ctypes.c_double(0.5)
+    for alg in (_lib.SPG_ALG1, _lib.SPG_ALG2):
+        wsb = ctypes.c_size_t(0)
+        _lib.check(lib.spg_plan(h.ptr, ctypes.byref(va), ctypes.byref(vb), alg, 0.2, ctypes.byref(wsb), None, None))
+        ws = torch.empty(wsb.value, dtype=torch.uint8, device=_dev())
+        indptr = torch.empty(4097, dtype=torch.int32, device=_dev())
+        nnz, peak = ctypes.c_int64(0), ctypes.c_size_t(0)
+        pj, px, plan = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        _lib.check(lib.spg_spgemm_ws(h.ptr, ctypes.byref(va), ctypes.byref(vb), alg, 0.2, ctypes.byref(al),
+                                     ctypes.c_void_p(ws.data_ptr()), wsb.value, ctypes.c_void_p(indptr.data_ptr()),
+                                     _lib.SPG_INDEX_32I, ctypes.byref(nnz), ctypes.byref(pj), ctypes.byref(px),
+                                     ctypes.byref(peak), ctypes.byref(plan)))
+        n = nnz.value
+        assert n == len(ref[1]) and peak.value > 0
+        if alg == _lib.SPG_ALG1:
+            assert pj.value and px.value and not plan.value
+            cj = ws[pj.value - ws.data_ptr():][:4 * n].view(torch.int32)
+            cx = ws[px.value - ws.data_ptr():][:8 * n].view(torch.float64)
+        else:
+            assert not pj.value and plan.value
+            cj = torch.empty(n, dtype=torch.int32, device=_dev())
+            cx = torch.empty(n, dtype=torch.float64, device=_dev())
+            vc = SpgCsr(4096, 4096, n, indptr.data_ptr(), cj.data_ptr(), cx.data_ptr(), _lib.SPG_INDEX_32I,
+                        _lib.SPG_R_64F)
+            _lib.check(lib.spg_numeric(h.ptr, plan, ctypes.byref(al), ctypes.byref(vc)))
+            lib.spg_plan_destroy(plan)
+        torch.cuda.synchronize()
+        _assert_same((indptr.cpu().numpy().astype(np.int64), cj.cpu().numpy(), cx.cpu().numpy()), ref)
