@@ -29,6 +29,8 @@
  *   - Stream ordering: every call enqueues on the handle's stream.  The only calls that
  *     wait on the device are spg_plan for ALG1/ALG3 (to size buffers from the product
  *     count), spg_num_products, spg_symbolic (nnz(C) to host) and spg_validate_csr.
+ *     spg_symbolic waits only for nnz(C): under ALG1 it returns while the numeric pass it
+ *     queued is still running, so C is ready in stream order, not on return.
  *   - Errors are status codes only; the library never calls exit().  SPG_STATUS_ALLOC_FAILED
  *     lets a harness print "[SKIP]" (dense_vs_sparseGEMM/utils.py:156-173).
  *   - A handle is not thread-safe: one handle per host thread per device (mirrors CuPy's
@@ -121,7 +123,7 @@ spg_status_t spg_create(spg_handle_t *handle, int hip_device);
 spg_status_t spg_destroy(spg_handle_t handle);
 
 /* Stream for all subsequent work (cusparseSetStream).  `stream` is a hipStream_t; NULL is
- * the null stream. */
+ * the null stream.  A change of stream first drains the old one. */
 spg_status_t spg_set_stream(spg_handle_t handle, void *stream);
 
 /* Last HIP error code seen by this handle (0 if none), for SPG_STATUS_HIP_ERROR. */

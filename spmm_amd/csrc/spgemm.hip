@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -22,7 +23,7 @@
 
 using namespace spg;
 
-constexpr int PINNED_WORDS = 16 + 1024;   // host-pinned scalars: 16 + per-chunk spill counts
+constexpr int PINNED_WORDS = MIRROR_GEN_WORD + 1;   // host-pinned: 16 scalars, per-chunk spill counts, generation
 
 struct spg_handle_s {
     int device = 0;
@@ -30,6 +31,7 @@ struct spg_handle_s {
     hipStream_t stream = nullptr;
     int last_hip = 0;
     int64_t* pinned = nullptr;      // PINNED_WORDS host-pinned int64 for device->host scalars
+    int64_t mirror_gen = 0;         // generation of the last scan that mirrors into `pinned`
     int32_t* spill_ctr = nullptr;   // ALG1 on k_row: spill counter, re-armed by the scan kernel
     bool spill_ctr_dirty = false;   // a count pass ran without its scan (re-zero first)
     void* scratch = nullptr;        // internal device scratch (plan-time analysis)
@@ -264,13 +266,13 @@ template <typename OUT>
 spg_status_t launch_scan(spg_handle_t h, int64_t n, const int64_t* in, OUT* out,
                          unsigned long long* status, int64_t* scal, bool zero_status,
                          int32_t* move_cnt = nullptr, int64_t* move_dst = nullptr,
-                         int64_t* host_mirror = nullptr) {
+                         int64_t* host_mirror = nullptr, int64_t mirror_gen = 0) {
     const int64_t tiles = scan_tiles(n);
     if (zero_status)
         SPG_HIP(h, hipMemsetAsync(status, 0, sizeof(unsigned long long) * (size_t)(tiles + 1), h->stream));
     PhaseTimer pt(h, SPG_PHASE_SCAN);
     hipLaunchKernelGGL(k_scan_lb<OUT>, dim3((unsigned)tiles), dim3(BLOCK), 0, h->stream, n, in, out,
-                       status, scal, move_cnt, move_dst, host_mirror);
+                       status, scal, move_cnt, move_dst, host_mirror, mirror_gen);
     SPG_LAUNCHED(h);
     return SPG_STATUS_SUCCESS;
 }
@@ -340,6 +342,27 @@ spg_status_t scratch_for_products(spg_handle_t h, int64_t rows, ScratchView& v) 
 
 // Waits for the handle's stream (polling hipStreamQuery measured slower on the box).
 hipError_t stream_wait(spg_handle_t h) { return hipStreamSynchronize(h->stream); }
+
+// Waits until the scan of generation h->mirror_gen has written its scalars to the pinned
+// buffer.  The numeric pass behind it stays queued on the stream: the call returns while it
+// runs (the results are stream-ordered, like every other output of the library).  A stream
+// that drains without the generation arriving, or reports an error, fails the call.
+spg_status_t wait_mirror(spg_handle_t h) {
+    const volatile int64_t* gen = (const volatile int64_t*)h->pinned + MIRROR_GEN_WORD;
+    for (unsigned spin = 1; *gen != h->mirror_gen; ++spin) {
+        if ((spin & 1023) == 0) {
+            const hipError_t e = hipStreamQuery(h->stream);
+            if (e == hipSuccess) {
+                if (*gen == h->mirror_gen) break;
+                return SPG_STATUS_EXECUTION_FAILED;
+            }
+            if (e != hipErrorNotReady) SPG_HIP(h, e);
+        }
+        __builtin_ia32_pause();
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    return SPG_STATUS_SUCCESS;
+}
 
 spg_status_t read_scalars(spg_handle_t h, const int64_t* dev, int n, int64_t* out) {
     if (n > PINNED_WORDS) return SPG_STATUS_INTERNAL_ERROR;
@@ -657,7 +680,8 @@ spg_status_t alg1_fused_run(spg_handle_t h, spg_plan_s& p, void* cp) {
                                (int)ROW_COUNT_ALL, (int64_t)0, (const int64_t*)nullptr, status, nstatus);
             SPG_LAUNCHED(h);
             spg_status_t st = launch_scan<OUT>(h, p.A.rows, (const int64_t*)p.row_cnt, (OUT*)cp, status,
-                                               p.scalars, false, h->spill_ctr, p.scalars + 5, h->pinned);
+                                               p.scalars, false, h->spill_ctr, p.scalars + 5, h->pinned,
+                                               ++h->mirror_gen);
             if (st) return st;
             h->spill_ctr_dirty = false;
         } else {   // repeated call: the first scan already moved the spill count
@@ -828,6 +852,7 @@ spg_status_t spg_create(spg_handle_t* handle, int hip_device) {
     h->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     hipError_t e = hipSetDevice(dev);
     if (e == hipSuccess) e = hipHostMalloc((void**)&h->pinned, PINNED_WORDS * sizeof(int64_t), hipHostMallocDefault);
+    if (e == hipSuccess) std::memset(h->pinned, 0, PINNED_WORDS * sizeof(int64_t));
     if (e == hipSuccess) e = hipMalloc((void**)&h->spill_ctr, 256);
     if (e == hipSuccess) e = hipMemset(h->spill_ctr, 0, 256);
     if (e != hipSuccess) {
@@ -840,10 +865,8 @@ spg_status_t spg_create(spg_handle_t* handle, int hip_device) {
 
 spg_status_t spg_destroy(spg_handle_t h) {
     if (!h) return SPG_STATUS_NOT_INITIALIZED;
-    if (h->scratch) {
-        (void)hipStreamSynchronize(h->stream);
-        (void)hipFree(h->scratch);
-    }
+    (void)hipStreamSynchronize(h->stream);   // an ALG1 call returns with its numeric pass queued
+    if (h->scratch) (void)hipFree(h->scratch);
     if (h->pinned) (void)hipHostFree(h->pinned);
     if (h->spill_ctr) (void)hipFree(h->spill_ctr);
     for (auto& q : h->pending) { (void)hipEventDestroy(q.a); (void)hipEventDestroy(q.b); }
@@ -854,6 +877,8 @@ spg_status_t spg_destroy(spg_handle_t h) {
 
 spg_status_t spg_set_stream(spg_handle_t h, void* stream) {
     if (!h) return SPG_STATUS_NOT_INITIALIZED;
+    // work still queued on the old stream may use the handle's scratch: drain it first
+    if ((hipStream_t)stream != h->stream) SPG_HIP(h, hipStreamSynchronize(h->stream));
     h->stream = (hipStream_t)stream;
     return SPG_STATUS_SUCCESS;
 }
@@ -999,9 +1024,9 @@ spg_status_t spg_symbolic(spg_handle_t h, spg_plan_t p, void* C_indptr, spg_inde
         if (st) return st;
         int64_t sc[6];
         if (!p->counts_ready) {
-            // the scan mirrored total / overflow / spills into the pinned buffer: wait for the
-            // stream (no device->host copy)
-            SPG_HIP(h, stream_wait(h));
+            // the scan mirrored total / overflow / spills into the pinned buffer: wait for
+            // that (no device->host copy, no wait for the numeric pass)
+            if ((st = wait_mirror(h))) return st;
             for (int i = 0; i < 6; ++i) sc[i] = ((volatile int64_t*)h->pinned)[i];
         } else if ((st = read_scalars(h, p->scalars, 6, sc))) {
             return st;

@@ -742,6 +742,9 @@ __global__ __launch_bounds__(G::WPB * WAVE, sizeof(T) <= 8 ? 5 : 2) void k_short
 // MI355X_MICROARCH.md, "Valid forms").
 constexpr int SCAN_ITEMS = 8;
 constexpr int SCAN_TILE = BLOCK * SCAN_ITEMS;   // 2048
+// word of the host-pinned buffer that carries the generation of the last mirrored scan (past
+// every word read_scalars fills)
+constexpr int MIRROR_GEN_WORD = 16 + 1024;
 
 template <typename OUT>
 __global__ __launch_bounds__(BLOCK) void k_scan_lb(int64_t n, const int64_t* __restrict__ in,
@@ -750,7 +753,8 @@ __global__ __launch_bounds__(BLOCK) void k_scan_lb(int64_t n, const int64_t* __r
                                                    int64_t* __restrict__ scalars,
                                                    int32_t* __restrict__ move_cnt = nullptr,
                                                    int64_t* __restrict__ move_dst = nullptr,
-                                                   int64_t* __restrict__ host_mirror = nullptr) {
+                                                   int64_t* __restrict__ host_mirror = nullptr,
+                                                   int64_t mirror_gen = 0) {
     constexpr unsigned long long VMASK = (1ull << 62) - 1;
     __shared__ long long wsum[WPB];
     __shared__ long long prefix_s;
@@ -832,6 +836,8 @@ __global__ __launch_bounds__(BLOCK) void k_scan_lb(int64_t n, const int64_t* __r
             __hip_atomic_store(&host_mirror[0], (int64_t)total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(&host_mirror[1], (int64_t)scalars[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(&host_mirror[5], moved, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            // the call's generation last: the host polls it instead of waiting for the stream
+            __hip_atomic_store(&host_mirror[MIRROR_GEN_WORD], mirror_gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
 }
