@@ -266,13 +266,13 @@ template <typename OUT>
 spg_status_t launch_scan(spg_handle_t h, int64_t n, const int64_t* in, OUT* out,
                          unsigned long long* status, int64_t* scal, bool zero_status,
                          int32_t* move_cnt = nullptr, int64_t* move_dst = nullptr,
-                         int64_t* host_mirror = nullptr, int64_t mirror_gen = 0) {
+                         int64_t* host_mirror = nullptr, int64_t mirror_gen = 0, int mirror_n = 0) {
     const int64_t tiles = scan_tiles(n);
     if (zero_status)
         SPG_HIP(h, hipMemsetAsync(status, 0, sizeof(unsigned long long) * (size_t)(tiles + 1), h->stream));
     PhaseTimer pt(h, SPG_PHASE_SCAN);
     hipLaunchKernelGGL(k_scan_lb<OUT>, dim3((unsigned)tiles), dim3(BLOCK), 0, h->stream, n, in, out,
-                       status, scal, move_cnt, move_dst, host_mirror, mirror_gen);
+                       status, scal, move_cnt, move_dst, host_mirror, mirror_gen, mirror_n);
     SPG_LAUNCHED(h);
     return SPG_STATUS_SUCCESS;
 }
@@ -635,7 +635,7 @@ spg_status_t run_numeric_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_t
 }
 
 template <typename OUT>
-spg_status_t run_scan(spg_handle_t h, spg_plan_s& p, void* out) {
+spg_status_t run_scan(spg_handle_t h, spg_plan_s& p, void* out, int mirror_n = 0) {
     if (p.use_tile) {
         // item counts -> item offsets in place (once: a repeated spg_symbolic reuses them);
         // C's row pointer = the offset of each row's first item (overflow of an int32 row
@@ -652,8 +652,10 @@ spg_status_t run_scan(spg_handle_t h, spg_plan_s& p, void* out) {
         return SPG_STATUS_SUCCESS;
     }
     // the row-pointer scan uses the second status region of the control block
+    // (mirror_n > 0: the control words also go to the pinned buffer, for wait_mirror)
     return launch_scan<OUT>(h, p.A.rows, (const int64_t*)p.row_cnt, (OUT*)out,
-                            p.scan_status + scan_tiles(p.A.rows) + 1, p.scalars, false);
+                            p.scan_status + scan_tiles(p.A.rows) + 1, p.scalars, false, nullptr, nullptr,
+                            mirror_n ? h->pinned : nullptr, mirror_n ? ++h->mirror_gen : 0, mirror_n);
 }
 
 // ALG1 single pass: structure + values + row pointer in one launch, compact into tj/tx
@@ -681,7 +683,7 @@ spg_status_t alg1_fused_run(spg_handle_t h, spg_plan_s& p, void* cp) {
             SPG_LAUNCHED(h);
             spg_status_t st = launch_scan<OUT>(h, p.A.rows, (const int64_t*)p.row_cnt, (OUT*)cp, status,
                                                p.scalars, false, h->spill_ctr, p.scalars + 5, h->pinned,
-                                               ++h->mirror_gen);
+                                               ++h->mirror_gen, 2);   // words 0, 1 (+ 5: the move)
             if (st) return st;
             h->spill_ctr_dirty = false;
         } else {   // repeated call: the first scan already moved the spill count
@@ -1138,18 +1140,26 @@ spg_status_t spg_symbolic(spg_handle_t h, spg_plan_t p, void* C_indptr, spg_inde
         }
         if (st) return st;
     }
-    st = C_indptr_type == SPG_INDEX_64I ? run_scan<int64_t>(h, *p, C_indptr)
-                                        : run_scan<int32_t>(h, *p, C_indptr);
+    // the row-pointer scan mirrors the control words (+ every chunk's spill count) into the
+    // pinned buffer: no device->host copy
+    const bool chunks = p->nspc > 0 && !p->counts_ready;
+    const int nread = chunks ? 16 + p->nspc : 5;
+    const bool mirror = !p->use_tile;
+    st = C_indptr_type == SPG_INDEX_64I ? run_scan<int64_t>(h, *p, C_indptr, mirror ? nread : 0)
+                                        : run_scan<int32_t>(h, *p, C_indptr, mirror ? nread : 0);
     if (st) return st;
+    std::vector<int64_t> all((size_t)nread);
+    if (mirror) {
+        if ((st = wait_mirror(h))) return st;
+        for (int i = 0; i < nread; ++i) all[(size_t)i] = ((volatile int64_t*)h->pinned)[i];
+    } else if ((st = read_scalars(h, p->scalars, nread, all.data()))) {
+        return st;
+    }
     int64_t sc[5];
-    if (p->nspc > 0 && !p->counts_ready) {   // scalars + every chunk's spill count, one read
-        std::vector<int64_t> all((size_t)(16 + p->nspc));
-        if ((st = read_scalars(h, p->scalars, (int)all.size(), all.data()))) return st;
-        for (int i = 0; i < 5; ++i) sc[i] = all[(size_t)i];
+    for (int i = 0; i < 5; ++i) sc[i] = all[(size_t)i];
+    if (chunks) {
         p->chunk_spills.assign(all.begin() + 16, all.end());
         for (auto& v : p->chunk_spills) v &= 0xffffffffLL;
-    } else if ((st = read_scalars(h, p->scalars, 5, sc))) {
-        return st;
     }
     // the short-row kernel spills the same rows in both passes: none in the symbolic pass
     // (one launch over all rows) means the numeric spill launch can be skipped

@@ -754,7 +754,7 @@ __global__ __launch_bounds__(BLOCK) void k_scan_lb(int64_t n, const int64_t* __r
                                                    int32_t* __restrict__ move_cnt = nullptr,
                                                    int64_t* __restrict__ move_dst = nullptr,
                                                    int64_t* __restrict__ host_mirror = nullptr,
-                                                   int64_t mirror_gen = 0) {
+                                                   int64_t mirror_gen = 0, int mirror_n = 0) {
     constexpr unsigned long long VMASK = (1ull << 62) - 1;
     __shared__ long long wsum[WPB];
     __shared__ long long prefix_s;
@@ -821,24 +821,39 @@ __global__ __launch_bounds__(BLOCK) void k_scan_lb(int64_t n, const int64_t* __r
         run += v[j];
     }
     const int64_t ntiles = n > 0 ? (n + SCAN_TILE - 1) / SCAN_TILE : 1;
-    if (bid == ntiles - 1 && tid == 0) {
+    if (bid != ntiles - 1) return;
+    if (tid == 0) {
         const long long total = prefix_s + btot;
         out[n] = (OUT)total;
+        const int64_t ovf = (sizeof(OUT) == 4 && total > 2147483647LL) ? 1 : 0;
         scalars[0] = total;
-        scalars[1] = (sizeof(OUT) == 4 && total > 2147483647LL) ? 1 : 0;
+        scalars[1] = ovf;
         int64_t moved = 0;
-        if (move_cnt) {   // (ALG1 on k_row) hand the spill count over and re-arm the counter
+        if (move_cnt) {   // (ALG1 on k_row) hand the spill count over (to scalars[5]) and re-arm
             moved = *move_cnt;
             *move_dst = moved;
             *move_cnt = 0;
         }
-        if (host_mirror) {   // total, overflow, spills straight to pinned host memory
+        // the control scalars (total, overflow, the symbolic pass's words, then the chunks'
+        // spill counts) to pinned host memory, one thread, 16 independent loads at a time (a
+        // block-wide system fence costs more than the few words a call has)
+        if (mirror_n > 0) {
             __hip_atomic_store(&host_mirror[0], (int64_t)total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(&host_mirror[1], (int64_t)scalars[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(&host_mirror[5], moved, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            // the call's generation last: the host polls it instead of waiting for the stream
-            __hip_atomic_store(&host_mirror[MIRROR_GEN_WORD], mirror_gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&host_mirror[1], ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (move_cnt) __hip_atomic_store(&host_mirror[5], moved, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
+        for (int b = 2; b < mirror_n; b += 16) {
+            int64_t w[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) w[i] = b + i < mirror_n ? scalars[b + i] : 0;
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                if (b + i < mirror_n)
+                    __hip_atomic_store(&host_mirror[b + i], w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        // the call's generation last: the host polls it instead of waiting for the stream
+        if (mirror_n > 0)
+            __hip_atomic_store(&host_mirror[MIRROR_GEN_WORD], mirror_gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
