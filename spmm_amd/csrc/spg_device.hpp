@@ -111,6 +111,18 @@ __device__ __forceinline__ int wave_incl_max_dpp(int v) {
     return v;
 }
 
+// Inclusive prefix max over the 64 lanes for unsigned values.  0 is max_u32's identity, so
+// each step folds into one v_max_u32_dpp (the signed form above needs a v_mov_b32_dpp too).
+__device__ __forceinline__ unsigned wave_incl_umax_dpp(unsigned v) {
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));
+    return v;
+}
+
 __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // Complex values (complex64 / complex128): two parts side by side, numpy's layout.  The

@@ -170,23 +170,25 @@ __device__ __forceinline__ void row_pass(Lds& S, int l, int cnt, int off, int P,
     if (l < G::NW / 32) S.dupw[l] = 0u;
 #pragma unroll
     for (int q = 0; q < (NC * WAVE + 511) / 512; ++q)
-        reinterpret_cast<uint64_t*>(S.mk)[q * WAVE + l] = ~0ull;
+        reinterpret_cast<uint64_t*>(S.mk)[q * WAVE + l] = 0ull;
     wsync();
-    if (cnt > 0) S.mk[off] = (int8_t)l;
+    if (cnt > 0) S.mk[off] = (int8_t)(l + 1);
     wsync();
-    // lane -> A entry of each product (marker bytes + DPP max scans carried across chunks)
-    int src[NC];
+    // lane -> A entry + 1 of each product (marker bytes + DPP max scans carried across
+    // chunks; the first product always has a marker, so every src >= 1)
+    unsigned src[NC];
     {
-        int mrk[NC];
+        unsigned mrk[NC];
 #pragma unroll
-        for (int r = 0; r < NC; ++r) mrk[r] = S.mk[r * WAVE + l];
-        int carry = -1;
+        for (int r = 0; r < NC; ++r) mrk[r] = (uint8_t)S.mk[r * WAVE + l];
+        unsigned carry = 0;
 #pragma unroll
         for (int r = 0; r < NC; ++r) {
-            src[r] = max(wave_incl_max_dpp(mrk[r]), carry);
-            carry = readlane_i(src[r], WAVE - 1);
+            src[r] = max(wave_incl_umax_dpp(mrk[r]), carry);
+            carry = (unsigned)readlane_i((int)src[r], WAVE - 1);
         }
     }
+    const JRec<T, IP, VALS>* jr1 = S.jr - 1;   // indexed by src
     IP idx[NC];
     T av[NC];
 #pragma unroll
@@ -194,10 +196,10 @@ __device__ __forceinline__ void row_pass(Lds& S, int l, int cnt, int off, int P,
         const int t = r * WAVE + l;
         JRec<T, IP, VALS> j;
         if constexpr (sizeof(j) == 16) {   // one ds_read_b128
-            const uint4 q = *reinterpret_cast<const uint4*>(&S.jr[src[r]]);
+            const uint4 q = *reinterpret_cast<const uint4*>(&jr1[src[r]]);
             __builtin_memcpy(&j, &q, 16);
         } else {
-            j = S.jr[src[r]];
+            j = jr1[src[r]];
         }
         idx[r] = t < P ? j.jb0 + (IP)(t - j.joff) : (IP)0;
         if constexpr (VALS) av[r] = j.ja;
@@ -218,21 +220,26 @@ __device__ __forceinline__ void row_pass(Lds& S, int l, int cnt, int off, int P,
         if (r * WAVE + l >= P) col[r] = -1;
     // column bits; a product whose bit was already set flags its word
     uint32_t dupb = 0;
+    int ndup = 0;   // products whose column was already set (wave total)
 #pragma unroll
     for (int r = 0; r < NC; ++r) {
         const int cc = col[r] < 0 ? 0 : col[r];
         const uint32_t bit = col[r] < 0 ? 0u : 1u << (cc & 31);
-        if (atomicOr(&S.bits[cc >> 5], bit) & bit) dupb |= 1u << r;
+        const bool hit = (atomicOr(&S.bits[cc >> 5], bit) & bit) != 0u;
+        if (hit) dupb |= 1u << r;
+        if (!VALS) ndup += (int)__popcll(__ballot(hit));
     }
-    const bool anydup = __ballot(dupb != 0u) != 0ull;
+    const bool anydup = VALS ? __ballot(dupb != 0u) != 0ull : ndup > 0;
     if (anydup) {
 #pragma unroll
         for (int r = 0; r < NC; ++r)
             if ((dupb >> r) & 1u) atomicOr(&S.dupw[col[r] >> 10], 1u << ((col[r] >> 5) & 31));
     }
     wsync();
+    // (counting) distinct columns = products - repeated hits: no bitmap popcount
+    if (!VALS) o.nnz = P - ndup;
     // popcount prefix over this lane's 8 contiguous words, word flags in bit 15
-    {
+    if constexpr (VALS) {
         const uint4 q0 = bits4[2 * l], q1 = bits4[2 * l + 1];
         const int c0 = __popc(q0.x), c1 = __popc(q0.y), c2 = __popc(q0.z), c3 = __popc(q0.w);
         const int c4 = __popc(q1.x), c5 = __popc(q1.y), c6 = __popc(q1.z), c7 = __popc(q1.w);
@@ -249,8 +256,8 @@ __device__ __forceinline__ void row_pass(Lds& S, int l, int cnt, int off, int P,
         w.z = f(p4, 4) | (f(p5, 5) << 16);
         w.w = f(p6, 6) | (f(p7, 7) << 16);
         reinterpret_cast<uint4*>(S.wpre)[l] = w;
+        wsync();
     }
-    wsync();
     // products in flagged words: their number decides the spill; (VALS) their list
     int L = 0;
 #pragma unroll
