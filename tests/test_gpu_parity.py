@@ -516,3 +516,48 @@ def test_spgemm_ws_abi():
             lib.spg_plan_destroy(plan)
         torch.cuda.synchronize()
         _assert_same((indptr.cpu().numpy().astype(np.int64), cj.cpu().numpy(), cx.cpu().numpy()), ref)
+
+
+def _oracle_ref(A, B):
+    return oracle.spgemm(A, B, keep_zeros=True, sort=True)
+
+
+@pytest.mark.parametrize("alg", [1, 2])
+def test_back_to_back_calls_stream_ordered(alg):
+    """ALG1/ALG2 calls return once nnz(C) is known, with the numeric pass still queued
+    (the scan mirrors its scalars into pinned memory).  Many back-to-back products with
+    different shapes, all results held, read only after one synchronize: each must match
+    its own oracle product."""
+    from spmm_amd import cusparse
+    from spmm_amd.sparse import csr_matrix
+    rng = np.random.default_rng(11)
+    cases, outs = [], []
+    for i in range(12):
+        n = int(rng.integers(200, 3000))
+        A = sp.random(n, n, density=float(rng.uniform(2e-3, 2e-2)), format="csr", random_state=100 + i)
+        B = sp.random(n, n, density=float(rng.uniform(2e-3, 2e-2)), format="csr", random_state=200 + i)
+        cases.append((A, B))
+        outs.append(cusparse.spgemm(csr_matrix(A, device=_dev()), csr_matrix(B, device=_dev()), alg=alg))
+    torch.cuda.synchronize()
+    for (A, B), C in zip(cases, outs):
+        got = (C.indptr.cpu().numpy().astype(np.int64), C.indices.cpu().numpy(), C.data.cpu().numpy())
+        _assert_same(got, _oracle_ref(A, B))
+
+
+def test_side_stream_and_stream_switch():
+    """A product issued on a side stream is ordered on that stream (the handle follows
+    torch's current stream; switching streams drains the old one first)."""
+    from spmm_amd import cusparse
+    from spmm_amd.sparse import csr_matrix
+    A = sp.random(4096, 4096, density=2e-3, format="csr", random_state=5)
+    B = sp.random(4096, 4096, density=2e-3, format="csr", random_state=6)
+    dA, dB = csr_matrix(A, device=_dev()), csr_matrix(B, device=_dev())
+    ref = _oracle_ref(A, B)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        C1 = cusparse.spgemm(dA, dB, alg=1)
+        got1 = (C1.indptr.cpu().numpy().astype(np.int64), C1.indices.cpu().numpy(), C1.data.cpu().numpy())
+    C2 = cusparse.spgemm(dA, dB, alg=1)   # back on the default stream
+    torch.cuda.synchronize()
+    _assert_same(got1, ref)
+    _assert_same((C2.indptr.cpu().numpy().astype(np.int64), C2.indices.cpu().numpy(), C2.data.cpu().numpy()), ref)
