@@ -54,13 +54,19 @@ std::tuple<int64_t, at::Tensor, at::Tensor, at::Tensor, int64_t, int64_t> spgemm
     size_t peak = 0;
     spg_plan_t plan = nullptr;
     at::Tensor indptr;
-    for (at::ScalarType it : {at::kInt, at::kLong}) {   // int64 row pointer once nnz(C) >= 2**31
+    // int64 row pointer once nnz(C) >= 2**31.  When the expected product count reaches 2**31
+    // the first try is int64 already (an int32 try that overflows would redo the plan and
+    // the symbolic pass); a result that fits is handed back with an int32 row pointer.
+    const double avg_b = k > 0 ? (double)B.nnz / (double)k : 0.0;
+    const bool wide = (double)A.nnz * avg_b >= 2147483648.0;
+    for (at::ScalarType it : {wide ? at::kLong : at::kInt, at::kLong}) {
         indptr = at::empty({m + 1}, opt.dtype(it));
         st = spg_spgemm_ws(h, &A, &B, a, cf, alpha, ws.data_ptr(), ws_bytes, indptr.data_ptr(), itype(indptr), &nnz,
                            &cj, &cx, &peak, &plan);
         if (st != SPG_STATUS_OVERFLOW) break;
     }
     if (st) return {st, {}, {}, {}, 0, 0};
+    const bool narrow = wide && nnz < 2147483648LL;   // back to the int32 contract
     at::Tensor indices, data;
     const int64_t vsz = Ax.element_size();
     if (cj) {   // ALG1: C sits compact (scaled) in the workspace
@@ -77,6 +83,7 @@ std::tuple<int64_t, at::Tensor, at::Tensor, at::Tensor, int64_t, int64_t> spgemm
         spg_plan_destroy(plan);
         if (st) return {st, {}, {}, {}, 0, 0};
     }
+    if (narrow) indptr = indptr.to(at::kInt);   // stream-ordered after the numeric pass
     return {0, data, indices, indptr, (int64_t)ws_bytes, (int64_t)peak};
 }
 

@@ -92,8 +92,11 @@ struct spg_plan_s {
     int64_t* cspill = nullptr;
     std::vector<int64_t> chunk_spills;
     int64_t cap = 0;                // ALG1 single pass: entries tj/tx hold (an estimate)
-    uint2* tidx = nullptr;          // B column-tile index, B.rows * G (start, end) pairs
-    void* brec = nullptr;           // B packed as (column, value) records (numeric tile pass)
+    uint2* tidx = nullptr;          // B column-tile index, B.rows * G (start, end) pairs (a
+                                    // temporary in the bitmap region, read before the symbolic pass)
+    int32_t* tptr = nullptr;        // tile-major B: segment table, G * (B.rows + 1)
+    uint32_t* sidx = nullptr;       // symbolic-tile starts inside each B row, B.rows * (Gs + 1)
+    void* brec = nullptr;           // tile-major B: (column, value) records (numeric tile pass)
     bool brec_built = false;
     uint32_t* bitmap = nullptr;     // per-item column bitmaps (symbolic -> numeric)
     int64_t* item_cnt = nullptr;    // per-item counts, scanned in place into offsets
@@ -113,10 +116,8 @@ inline size_t vbytes(spg_dtype_t t) {
     return t == SPG_C_64F ? 16 : (t == SPG_R_64F || t == SPG_C_32F) ? 8 : 4;
 }
 
-// bytes of one packed B record (BRec<T>) of the tile path
-inline size_t brec_bytes(spg_dtype_t t) {
-    return t == SPG_C_64F ? 24 : (t == SPG_R_64F || t == SPG_C_32F) ? 16 : 8;
-}
+// bytes of one tile-major B record of the tile path (column in tile + value, unpadded)
+inline size_t brec_bytes(spg_dtype_t t) { return 4 + vbytes(t); }
 
 // Runs f(T{}) with T the C++ type of value type t.
 template <typename F>
@@ -138,6 +139,22 @@ inline bool row_kernel_enabled() {
         return !(e && std::strcmp(e, "short") == 0);
     }();
     return on;
+}
+
+// Tile numeric kernel variant (A/B timing): SPG_TILE_RU = chunks per owner-round group
+// (1, 2, or all in flight), SPG_TILE_DENSE=0 turns the column-addressed accumulator off.
+struct TileVariant { int ru; bool dense; int diag; };
+inline const TileVariant& tile_variant() {
+    static const TileVariant v = [] {
+        TileVariant t{1, true, 0};
+        if (const char* e = std::getenv("SPG_TILE_RU")) t.ru = std::atoi(e);
+        if (const char* e = std::getenv("SPG_TILE_DENSE")) t.dense = std::atoi(e) != 0;
+        // timing-only diagnostics (results wrong): 1 = no accumulation, 2 = no record loads,
+        // 4 = no product batches, 8 = no output stores (dense tiles)
+        if (const char* e = std::getenv("SPG_TILE_DIAG")) t.diag = std::atoi(e);
+        return t;
+    }();
+    return v;
 }
 
 inline int64_t grid_for(int64_t rows, int per_block) { return (rows + per_block - 1) / per_block; }
@@ -168,7 +185,14 @@ inline bool want_tile(const spg_csr_t& A, const spg_csr_t& B, int& tws, int& G) 
         if (tw <= TILE_CAP || frac * tw <= 0.95 * TILE_CAP) tws = t;
         if (tw >= (double)B.cols) break;
     }
+    if (const char* e = std::getenv("SPG_TILE_TWS")) {   // A/B timing: force the tile width
+        const int t = std::atoi(e);
+        if (t >= 8 && t <= 12) tws = t;
+    }
     if (frac * (double)(1 << tws) < 64.0) return false;
+    // the tile-major B's segment table is int32 and its records are addressed with 32-bit
+    // byte offsets
+    if (B.nnz > 2147483647LL || (double)B.nnz * (double)brec_bytes(B.value_type) >= 4294967296.0) return false;
     G = (int)((B.cols + (1 << tws) - 1) >> tws);
     return (double)A.rows * G < 2.0e9;
 }
@@ -262,17 +286,18 @@ spg_status_t ensure_scratch(spg_handle_t h, size_t bytes) {
 
 // Product prefix of every row into `pref` (rows + 1 int64) and its total into scal[0].
 // `status` (tiles + 1 words) must be zero: plans zero theirs once when they are built
-template <typename OUT>
-spg_status_t launch_scan(spg_handle_t h, int64_t n, const int64_t* in, OUT* out,
+template <typename OUT, typename IN = int64_t>
+spg_status_t launch_scan(spg_handle_t h, int64_t n, const IN* in, OUT* out,
                          unsigned long long* status, int64_t* scal, bool zero_status,
                          int32_t* move_cnt = nullptr, int64_t* move_dst = nullptr,
-                         int64_t* host_mirror = nullptr, int64_t mirror_gen = 0, int mirror_n = 0) {
+                         int64_t* host_mirror = nullptr, int64_t mirror_gen = 0, int mirror_n = 0,
+                         const int64_t* seed = nullptr) {
     const int64_t tiles = scan_tiles(n);
     if (zero_status)
         SPG_HIP(h, hipMemsetAsync(status, 0, sizeof(unsigned long long) * (size_t)(tiles + 1), h->stream));
     PhaseTimer pt(h, SPG_PHASE_SCAN);
-    hipLaunchKernelGGL(k_scan_lb<OUT>, dim3((unsigned)tiles), dim3(BLOCK), 0, h->stream, n, in, out,
-                       status, scal, move_cnt, move_dst, host_mirror, mirror_gen, mirror_n);
+    hipLaunchKernelGGL((k_scan_lb<OUT, IN>), dim3((unsigned)tiles), dim3(BLOCK), 0, h->stream, n, in, out,
+                       status, scal, move_cnt, move_dst, host_mirror, mirror_gen, mirror_n, seed);
     SPG_LAUNCHED(h);
     return SPG_STATUS_SUCCESS;
 }
@@ -374,23 +399,43 @@ spg_status_t read_scalars(spg_handle_t h, const int64_t* dev, int n, int64_t* ou
 
 struct Layout {
     size_t scalars = 0, row_cnt = 0, seg = 0, spill = 0, status = 0, ub = 0, tj = 0, tx = 0;
-    size_t tidx = 0, items = 0, bitmap = 0, brec = 0, total = 0;
+    size_t tptr = 0, sidx = 0, items = 0, bitmap = 0, brec = 0, total = 0;
 };
 
-inline int64_t tile_items(const spg_plan_s& p) { return p.use_tile ? p.A.rows * p.G : 0; }
+// Tile path row chunks: ALG3's chunks (items and bitmaps are sized by the largest one and
+// reused chunk by chunk -- the working set ALG3 caps), otherwise all rows in one.
+inline int64_t tile_chunks(const spg_plan_s& p) {
+    return p.alg == SPG_ALG3 && p.chunk_rows.size() > 1 ? (int64_t)p.chunk_rows.size() - 1 : 1;
+}
+inline int64_t tile_chunk_r0(const spg_plan_s& p, int64_t c) { return tile_chunks(p) > 1 ? p.chunk_rows[(size_t)c] : 0; }
+inline int64_t tile_chunk_r1(const spg_plan_s& p, int64_t c) {
+    return tile_chunks(p) > 1 ? p.chunk_rows[(size_t)c + 1] : p.A.rows;
+}
+inline int64_t tile_rows_max(const spg_plan_s& p) {
+    int64_t mx = 0;
+    for (int64_t c = 0; c < tile_chunks(p); ++c) mx = std::max(mx, tile_chunk_r1(p, c) - tile_chunk_r0(p, c));
+    return mx;
+}
+inline int64_t tile_items(const spg_plan_s& p) { return p.use_tile ? tile_rows_max(p) * p.G : 0; }
+inline int sym_tiles(const spg_plan_s& p) { const int R = 1 << (p.twss - p.tws); return (p.G + R - 1) / R; }
+inline int64_t bt_entries(const spg_plan_s& p) { return p.use_tile ? (int64_t)p.G * (p.B.rows + 1) : 0; }
 
 // ALG1 runs as one fused pass (k_short SHORT_NUMLB) when the short-row kernel takes the shape
 inline bool fused_alg1(const spg_plan_s& p) {
     return p.alg == SPG_ALG1 && p.use_short && !p.use_tile && p.A.rows <= (1LL << 24);
 }
 
-// status words: products scan | row-pointer scan | item scan (tile path)
+// status words: products scan | row-pointer scan | item scan + segment-table scan (tile path)
 inline size_t status_words(const spg_plan_s& p) {
-    return 2 * (size_t)(scan_tiles(p.A.rows) + 1) + (p.use_tile ? (size_t)scan_tiles(tile_items(p)) + 1 : 0) +
+    return 2 * (size_t)(scan_tiles(p.A.rows) + 1) +
+           (p.use_tile ? (size_t)scan_tiles(tile_items(p)) + 1 + (size_t)scan_tiles(bt_entries(p)) + 1 : 0) +
            (fused_alg1(p) ? (size_t)grid_for(p.A.rows, ShortSmall::WPB) + 1 : 0);
 }
 inline unsigned long long* item_scan_status(const spg_plan_s& p) {
     return p.scan_status + 2 * (scan_tiles(p.A.rows) + 1);
+}
+inline unsigned long long* bt_scan_status(const spg_plan_s& p) {
+    return item_scan_status(p) + scan_tiles(tile_items(p)) + 1;
 }
 
 Layout make_layout(const spg_plan_s& p) {
@@ -402,10 +447,15 @@ Layout make_layout(const spg_plan_s& p) {
     L.seg = off;     off = align_up(off + sizeof(uint32_t) * 2 * (size_t)std::max<int64_t>(p.seg_len, 1));
     L.spill = off;   off = align_up(off + sizeof(int32_t) * 2 * (size_t)std::max<int64_t>(p.A.rows, 1));
     if (p.use_tile) {
-        L.tidx = off;  off = align_up(off + sizeof(uint2) * (size_t)p.B.rows * (size_t)p.G);
+        L.tptr = off;  off = align_up(off + sizeof(int32_t) * (size_t)(bt_entries(p) + 1));
+        L.sidx = off;  off = align_up(off + sizeof(uint32_t) * (size_t)p.B.rows * (size_t)(sym_tiles(p) + 1));
         L.brec = off;  off = align_up(off + brec_bytes(p.A.value_type) * (size_t)std::max<int64_t>(p.B.nnz, 1));
         L.items = off; off = align_up(off + sizeof(int64_t) * (size_t)(tile_items(p) + 1));
-        L.bitmap = off; off = align_up(off + sizeof(uint32_t) * (size_t)tile_items(p) * (size_t)((1 << p.tws) >> 5));
+        // item bitmaps; before the first symbolic pass the region holds the row-major
+        // boundary index the tile-major B is built from
+        const size_t bm = sizeof(uint32_t) * (size_t)tile_items(p) * (size_t)((1 << p.tws) >> 5);
+        const size_t ti = sizeof(uint2) * (size_t)p.B.rows * (size_t)p.G;
+        L.bitmap = off; off = align_up(off + std::max(bm, ti));
     }
     if (p.alg == SPG_ALG1 && !p.use_tile) {
         // single pass: C itself, `cap` entries (an estimate); upper-bound path: P entries
@@ -427,7 +477,9 @@ void carve(spg_plan_s& p, const Layout& L) {
     p.scan_status = (unsigned long long*)(p.ws + L.status);
     if (fused_alg1(p)) p.lb = p.scan_status + 2 * (scan_tiles(p.A.rows) + 1);
     if (p.use_tile) {
-        p.tidx = (uint2*)(p.ws + L.tidx);
+        p.tptr = (int32_t*)(p.ws + L.tptr);
+        p.sidx = (uint32_t*)(p.ws + L.sidx);
+        p.tidx = (uint2*)(p.ws + L.bitmap);
         p.brec = (void*)(p.ws + L.brec);
         p.item_cnt = (int64_t*)(p.ws + L.items);
         p.bitmap = (uint32_t*)(p.ws + L.bitmap);
@@ -503,18 +555,7 @@ spg_status_t run_symbolic_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_
     const int32_t* Aj = (const int32_t*)p.A.indices;
     const int32_t* Bj = (const int32_t*)p.B.indices;
     if (p.use_tile) {
-        if (!p.tidx_built) {
-            PhaseTimer ps(h, SPG_PHASE_SPILL);
-            hipLaunchKernelGGL(k_tile_index<IP>, dim3((unsigned)grid_for(p.B.rows, 4)), dim3(256), 0,
-                               h->stream, p.B.rows, Bp, Bj, p.tws, p.G, p.tidx);
-            SPG_LAUNCHED(h);
-            p.tidx_built = true;
-        }
-        PhaseTimer pt(h, SPG_PHASE_SYMBOLIC);
-        const int R = 1 << (p.twss - p.tws);
-        hipLaunchKernelGGL(k_tile_sym<IP>, dim3(tile_grid(n * ((p.G + R - 1) / R))), dim3(TILE_WPB * WAVE), 0,
-                           h->stream, r0, n, p.tws, p.G, p.twss, Ap, Aj, Bp, Bj, (const uint2*)p.tidx,
-                           p.bitmap, p.item_cnt);
+        return SPG_STATUS_INTERNAL_ERROR;   // the tile path runs through tile_symbolic
     } else if (p.use_short && p.nspc > 0) {
         // k_row counts every row (spills by the chunked loop) and lists this chunk's spills
         PhaseTimer pt(h, SPG_PHASE_SYMBOLIC);
@@ -573,17 +614,7 @@ spg_status_t run_numeric_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_t
     const T* Bx = (const T*)p.B.values;
     constexpr int MODE = UB ? SHORT_NUMUB : SHORT_NUM;
     if (p.use_tile) {
-        if (!p.brec_built) {
-            PhaseTimer ps(h, SPG_PHASE_SPILL);
-            hipLaunchKernelGGL(k_pack_b<T>, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(grid_for(p.B.nnz, 256), 8192))),
-                               dim3(256), 0, h->stream, p.B.nnz, Bj, Bx, (BRec<T>*)p.brec);
-            SPG_LAUNCHED(h);
-            p.brec_built = true;
-        }
-        PhaseTimer pt(h, SPG_PHASE_NUMERIC);
-        hipLaunchKernelGGL((k_tile<T, IP>), dim3(tile_grid(n * p.G)), dim3(TILE_WPB * WAVE), 0, h->stream, r0,
-                           n, p.tws, p.G, Ap, Aj, Ax, Bp, (const BRec<T>*)p.brec, (const uint2*)p.tidx,
-                           (const uint32_t*)p.bitmap, (const int64_t*)p.item_cnt, cj, cx, alpha);
+        return SPG_STATUS_INTERNAL_ERROR;   // the tile path runs through tile_numeric
     } else if (p.use_short && p.nspc > 0 && !UB) {
         {
             PhaseTimer pt(h, SPG_PHASE_NUMERIC);
@@ -636,26 +667,136 @@ spg_status_t run_numeric_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_t
 
 template <typename OUT>
 spg_status_t run_scan(spg_handle_t h, spg_plan_s& p, void* out, int mirror_n = 0) {
-    if (p.use_tile) {
-        // item counts -> item offsets in place (once: a repeated spg_symbolic reuses them);
-        // C's row pointer = the offset of each row's first item (overflow of an int32 row
-        // pointer is checked on the host)
-        if (!p.counts_ready) {
-            spg_status_t st = launch_scan<int64_t>(h, tile_items(p), (const int64_t*)p.item_cnt, p.item_cnt,
-                                                   item_scan_status(p), p.scalars, false);
-            if (st) return st;
-        }
-        PhaseTimer pt(h, SPG_PHASE_SCAN);
-        hipLaunchKernelGGL(k_items_to_rowptr<OUT>, dim3((unsigned)grid_for(p.A.rows + 1, 256)), dim3(256), 0,
-                           h->stream, p.A.rows, p.G, (const int64_t*)p.item_cnt, (OUT*)out);
-        SPG_LAUNCHED(h);
-        return SPG_STATUS_SUCCESS;
-    }
     // the row-pointer scan uses the second status region of the control block
     // (mirror_n > 0: the control words also go to the pinned buffer, for wait_mirror)
     return launch_scan<OUT>(h, p.A.rows, (const int64_t*)p.row_cnt, (OUT*)out,
                             p.scan_status + scan_tiles(p.A.rows) + 1, p.scalars, false, nullptr, nullptr,
                             mirror_n ? h->pinned : nullptr, mirror_n ? ++h->mirror_gen : 0, mirror_n);
+}
+
+// ------------------------------------------------------------------------ tile path
+// Once per plan: the row-major boundary index (a temporary in the bitmap region) -> the
+// tile-major segment table + symbolic-tile starts.
+template <typename IP>
+spg_status_t tile_build_index(spg_handle_t h, spg_plan_s& p) {
+    if (p.tidx_built) return SPG_STATUS_SUCCESS;
+    const IP* Bp = (const IP*)p.B.indptr;
+    const int32_t* Bj = (const int32_t*)p.B.indices;
+    const int R = 1 << (p.twss - p.tws);
+    {
+        PhaseTimer ps(h, SPG_PHASE_SPILL);
+        hipLaunchKernelGGL(k_tile_index<IP>, dim3((unsigned)grid_for(p.B.rows, 4)), dim3(256), 0, h->stream,
+                           p.B.rows, Bp, Bj, p.tws, p.G, p.tidx);
+        SPG_LAUNCHED(h);
+        const int64_t n2 = p.B.rows * p.G + p.G;
+        hipLaunchKernelGGL(k_bt_count, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(grid_for(n2, 256), 65536))),
+                           dim3(256), 0, h->stream, p.B.rows, p.G, R, (const uint2*)p.tidx, p.tptr, p.sidx);
+        SPG_LAUNCHED(h);
+    }
+    spg_status_t st = launch_scan<int32_t, int32_t>(h, bt_entries(p), p.tptr, p.tptr, bt_scan_status(p),
+                                                    p.scalars + 2, false);
+    if (st) return st;
+    p.tidx_built = true;
+    return SPG_STATUS_SUCCESS;
+}
+
+// Symbolic tiles of chunk c -> its item counts and bitmaps, then the item offsets (a scan
+// seeded with the previous chunk's total: offsets are C positions) and its rows' part of
+// C's row pointer.  Totals alternate between two scalar slots; the last chunk's lands in
+// scalars[0..1] (total, overflow), where spg_symbolic reads it.
+template <typename IP>
+spg_status_t tile_sym_chunk(spg_handle_t h, spg_plan_s& p, int64_t c) {
+    const int64_t r0 = tile_chunk_r0(p, c), n = tile_chunk_r1(p, c) - r0;
+    if (n > 0) {
+        PhaseTimer pt(h, SPG_PHASE_SYMBOLIC);
+        hipLaunchKernelGGL(k_tile_sym<IP>, dim3(tile_grid(n * sym_tiles(p))), dim3(TILE_WPB * WAVE), 0, h->stream,
+                           r0, n, p.tws, p.G, p.twss, (const IP*)p.A.indptr, (const int32_t*)p.A.indices,
+                           (const IP*)p.B.indptr, (const int32_t*)p.B.indices, (const uint32_t*)p.sidx, p.bitmap,
+                           p.item_cnt);
+        SPG_LAUNCHED(h);
+    }
+    const int64_t nch = tile_chunks(p);
+    int64_t* scal = c == nch - 1 ? p.scalars : p.scalars + 12 + 2 * (c & 1);
+    const int64_t* seed = c == 0 ? nullptr : p.scalars + 12 + 2 * ((c - 1) & 1);
+    return launch_scan<int64_t>(h, n * p.G, (const int64_t*)p.item_cnt, p.item_cnt, item_scan_status(p), scal,
+                                true, nullptr, nullptr, nullptr, 0, 0, seed);
+}
+
+template <typename OUT>
+spg_status_t tile_rowptr_chunk(spg_handle_t h, spg_plan_s& p, int64_t c, void* cp) {
+    const int64_t r0 = tile_chunk_r0(p, c), n = tile_chunk_r1(p, c) - r0;
+    PhaseTimer pt(h, SPG_PHASE_SCAN);
+    hipLaunchKernelGGL(k_items_to_rowptr<OUT>, dim3((unsigned)grid_for(n + 1, 256)), dim3(256), 0, h->stream, n,
+                       p.G, (const int64_t*)p.item_cnt, (OUT*)cp + r0);
+    SPG_LAUNCHED(h);
+    return SPG_STATUS_SUCCESS;
+}
+
+// spg_symbolic on the tile path: every chunk's counts, offsets and row pointer.  A single
+// chunk's offsets stay valid for the numeric pass (and a repeated call only rewrites the
+// row pointer); with several chunks the numeric pass recomputes each chunk's.
+template <typename IP, typename OUT>
+spg_status_t tile_symbolic(spg_handle_t h, spg_plan_s& p, void* cp) {
+    spg_status_t st;
+    if ((st = tile_build_index<IP>(h, p))) return st;
+    const int64_t nch = tile_chunks(p);
+    if (nch == 1 && p.counts_ready) return tile_rowptr_chunk<OUT>(h, p, 0, cp);
+    for (int64_t c = 0; c < nch; ++c) {
+        if ((st = tile_sym_chunk<IP>(h, p, c))) return st;
+        if ((st = tile_rowptr_chunk<OUT>(h, p, c, cp))) return st;
+    }
+    return SPG_STATUS_SUCCESS;
+}
+
+// spg_numeric on the tile path: the tile-major B records once, then chunk by chunk (the
+// chunk's counts, bitmaps and offsets again when there are several) the numeric tiles.
+template <typename T, typename IP>
+spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T alpha) {
+    const IP* Ap = (const IP*)p.A.indptr;
+    const IP* Bp = (const IP*)p.B.indptr;
+    const int32_t* Aj = (const int32_t*)p.A.indices;
+    const int32_t* Bj = (const int32_t*)p.B.indices;
+    const T* Ax = (const T*)p.A.values;
+    const T* Bx = (const T*)p.B.values;
+    if (!p.brec_built) {
+        PhaseTimer ps(h, SPG_PHASE_SPILL);
+        hipLaunchKernelGGL((k_bt_pack<T, IP>), dim3((unsigned)grid_for(p.B.rows, 4)), dim3(256), 0, h->stream,
+                           p.B.rows, Bp, Bj, Bx, p.tws, (const int32_t*)p.tptr, (uint32_t*)p.brec);
+        SPG_LAUNCHED(h);
+        p.brec_built = true;
+    }
+    const int64_t nch = tile_chunks(p);
+    for (int64_t c = 0; c < nch; ++c) {
+        spg_status_t st;
+        if (nch > 1 && (st = tile_sym_chunk<IP>(h, p, c))) return st;
+        const int64_t r0 = tile_chunk_r0(p, c), n = tile_chunk_r1(p, c) - r0;
+        if (n <= 0) continue;
+        PhaseTimer pt(h, SPG_PHASE_NUMERIC);
+        // dense accumulator when the tile fits one window; round groups (tile_variant())
+        const bool dense = (1 << p.tws) <= TILE_CAP && tile_variant().dense;
+        const int ru = tile_variant().ru;
+        auto launch = [&](auto dn, auto rn) {
+            constexpr bool DN = decltype(dn)::value;
+            constexpr int RN = decltype(rn)::value;
+            hipLaunchKernelGGL((k_tile<T, IP, DN, RN>), dim3(tile_grid(n * p.G)), dim3(TILE_WPB * WAVE), 0, h->stream,
+                               r0, n, p.tws, p.G, Ap, Aj, Ax, p.B.rows, (const uint32_t*)p.brec,
+                               (const int32_t*)p.tptr, (const uint32_t*)p.bitmap, (const int64_t*)p.item_cnt,
+                               cj, cx, alpha, tile_variant().diag);
+        };
+        constexpr int UF = sizeof(T) > 8 ? 4 : 8;
+        using D1 = std::integral_constant<bool, true>;
+        using D0 = std::integral_constant<bool, false>;
+        using R1 = std::integral_constant<int, 1>;
+        using R2 = std::integral_constant<int, 2>;
+        using RF = std::integral_constant<int, UF>;
+        if (dense) {
+            if (ru == 2) launch(D1{}, R2{}); else if (ru >= UF) launch(D1{}, RF{}); else launch(D1{}, R1{});
+        } else {
+            if (ru == 2) launch(D0{}, R2{}); else if (ru >= UF) launch(D0{}, RF{}); else launch(D0{}, R1{});
+        }
+        SPG_LAUNCHED(h);
+    }
+    return SPG_STATUS_SUCCESS;
 }
 
 // ALG1 single pass: structure + values + row pointer in one launch, compact into tj/tx
@@ -784,6 +925,7 @@ spg_status_t numeric_typed(spg_handle_t h, spg_plan_s& p, const spg_csr_t& C, T 
         return SPG_STATUS_SUCCESS;
     }
     spg_status_t st;
+    if (p.use_tile) return tile_numeric<T, IP>(h, p, (int32_t*)C.indices, (T*)C.values, alpha);
     if (p.alg == SPG_ALG3) {
         for (size_t c = 0; c + 1 < p.chunk_rows.size(); ++c) {
             if (c > 0 && p.use_short && p.nspc == 0)
@@ -1123,6 +1265,24 @@ spg_status_t spg_symbolic(spg_handle_t h, spg_plan_t p, void* C_indptr, spg_inde
         p->fused_failed = true;
         p->symbolic_runs = 0;
     }
+    if (p->use_tile) {
+        // counts, offsets and row pointer chunk by chunk; the last scan leaves the total in
+        // scalars[0] (overflow of an int32 row pointer is checked here)
+        st = i64 ? (C_indptr_type == SPG_INDEX_64I ? tile_symbolic<int64_t, int64_t>(h, *p, C_indptr)
+                                                   : tile_symbolic<int64_t, int32_t>(h, *p, C_indptr))
+                 : (C_indptr_type == SPG_INDEX_64I ? tile_symbolic<int32_t, int64_t>(h, *p, C_indptr)
+                                                   : tile_symbolic<int32_t, int32_t>(h, *p, C_indptr));
+        if (st) return st;
+        int64_t tot;
+        if ((st = read_scalars(h, p->scalars, 1, &tot))) return st;
+        p->counts_ready = true;
+        if (C_indptr_type == SPG_INDEX_32I && tot > 2147483647LL) return SPG_STATUS_OVERFLOW;
+        p->nnzC = tot;
+        p->c_indptr = C_indptr;
+        p->c_indptr_type = C_indptr_type;
+        *nnzC = tot;
+        return SPG_STATUS_SUCCESS;
+    }
     if (p->symbolic_runs++ > 0 && !p->use_tile) {
         // a repeated call (e.g. retrying with int64 row pointers): the row counts are kept;
         // re-arm the row-pointer scan's status words
@@ -1144,17 +1304,12 @@ spg_status_t spg_symbolic(spg_handle_t h, spg_plan_t p, void* C_indptr, spg_inde
     // pinned buffer: no device->host copy
     const bool chunks = p->nspc > 0 && !p->counts_ready;
     const int nread = chunks ? 16 + p->nspc : 5;
-    const bool mirror = !p->use_tile;
-    st = C_indptr_type == SPG_INDEX_64I ? run_scan<int64_t>(h, *p, C_indptr, mirror ? nread : 0)
-                                        : run_scan<int32_t>(h, *p, C_indptr, mirror ? nread : 0);
+    st = C_indptr_type == SPG_INDEX_64I ? run_scan<int64_t>(h, *p, C_indptr, nread)
+                                        : run_scan<int32_t>(h, *p, C_indptr, nread);
     if (st) return st;
     std::vector<int64_t> all((size_t)nread);
-    if (mirror) {
-        if ((st = wait_mirror(h))) return st;
-        for (int i = 0; i < nread; ++i) all[(size_t)i] = ((volatile int64_t*)h->pinned)[i];
-    } else if ((st = read_scalars(h, p->scalars, nread, all.data()))) {
-        return st;
-    }
+    if ((st = wait_mirror(h))) return st;
+    for (int i = 0; i < nread; ++i) all[(size_t)i] = ((volatile int64_t*)h->pinned)[i];
     int64_t sc[5];
     for (int i = 0; i < 5; ++i) sc[i] = all[(size_t)i];
     if (chunks) {
@@ -1164,9 +1319,8 @@ spg_status_t spg_symbolic(spg_handle_t h, spg_plan_t p, void* C_indptr, spg_inde
     // the short-row kernel spills the same rows in both passes: none in the symbolic pass
     // (one launch over all rows) means the numeric spill launch can be skipped
     if (p->use_short && (p->alg == SPG_ALG2 || fused_alg1(*p))) p->sym_spills = (int64_t)(uint32_t)(sc[4] & 0xffffffffu);
-    p->counts_ready = true;      // counts (and tile offsets) stay valid for a repeated call
-    if (sc[1] || (p->use_tile && C_indptr_type == SPG_INDEX_32I && sc[0] > 2147483647LL))
-        return SPG_STATUS_OVERFLOW;
+    p->counts_ready = true;      // counts stay valid for a repeated call
+    if (sc[1]) return SPG_STATUS_OVERFLOW;
     p->nnzC = sc[0];
     p->c_indptr = C_indptr;
     p->c_indptr_type = C_indptr_type;

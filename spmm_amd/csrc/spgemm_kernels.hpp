@@ -734,7 +734,8 @@ __global__ __launch_bounds__(G::WPB * WAVE, sizeof(T) <= 8 ? 5 : 2) void k_short
 
 // ---------------------------------------------------------------------------------------
 // Single-pass exclusive scan with decoupled look-back.  out[0..n) = exclusive prefix of
-// in[], out[n] = total, scalars[0] = total, scalars[1] = 1 if the total overflows OUT.
+// in[] (plus *seed when given), out[n] = total, scalars[0] = total, scalars[1] = 1 if the
+// total overflows OUT.
 // `status` holds 1 ticket word + one 8-byte status per tile and must be zero on entry.
 // Status word: bits 63..62 = 0 not ready / 1 tile aggregate / 2 inclusive prefix,
 // bits 61..0 = value.  Tiles take tickets in order, so every tile a block waits on has
@@ -746,15 +747,15 @@ constexpr int SCAN_TILE = BLOCK * SCAN_ITEMS;   // 2048
 // every word read_scalars fills)
 constexpr int MIRROR_GEN_WORD = 16 + 1024;
 
-template <typename OUT>
-__global__ __launch_bounds__(BLOCK) void k_scan_lb(int64_t n, const int64_t* __restrict__ in,
-                                                   OUT* __restrict__ out,
+template <typename OUT, typename IN = int64_t>
+__global__ __launch_bounds__(BLOCK) void k_scan_lb(int64_t n, const IN* in, OUT* out,
                                                    unsigned long long* __restrict__ status,
                                                    int64_t* __restrict__ scalars,
                                                    int32_t* __restrict__ move_cnt = nullptr,
                                                    int64_t* __restrict__ move_dst = nullptr,
                                                    int64_t* __restrict__ host_mirror = nullptr,
-                                                   int64_t mirror_gen = 0, int mirror_n = 0) {
+                                                   int64_t mirror_gen = 0, int mirror_n = 0,
+                                                   const int64_t* seed = nullptr) {
     constexpr unsigned long long VMASK = (1ull << 62) - 1;
     __shared__ long long wsum[WPB];
     __shared__ long long prefix_s;
@@ -784,8 +785,9 @@ __global__ __launch_bounds__(BLOCK) void k_scan_lb(int64_t n, const int64_t* __r
     if (wv == 0) {
         long long prefix = 0;
         if (bid == 0) {
+            if (seed) prefix = *seed;   // a chunked scan continues from the previous chunk's total
             if (l == 0)
-                __hip_atomic_store(&st[0], (2ull << 62) | (unsigned long long)btot, __ATOMIC_RELAXED,
+                __hip_atomic_store(&st[0], (2ull << 62) | (unsigned long long)(prefix + btot), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
         } else {
             if (l == 0)

@@ -28,7 +28,7 @@ template <typename T, typename IP, bool VALS> struct TileLds {
     T ja[WAVE];
     IP jb0[WAVE];
     uint32_t joff[WAVE];
-    int8_t mk[TILE_MK];
+    uint8_t mk[TILE_MK];
 };
 
 // Numeric tile pass LDS: the bitmap word and its popcount prefix side by side (one 8-byte
@@ -43,7 +43,7 @@ template <typename T, typename IP> struct NumLds {
     T acc[TILE_CAP];
     uint32_t tag[TILE_CAP];
     TileEnt<T, IP> ent[WAVE];
-    int8_t mk[TILE_MK];
+    uint8_t mk[TILE_MK];
 };
 
 // ---------------------------------------------------------------------------------------
@@ -78,38 +78,105 @@ __global__ __launch_bounds__(256) void k_tile_index(int64_t rows, const IP* __re
     for (int g = tl + 1 + l; g <= G; g += WAVE) put(g, (uint32_t)len);
 }
 
-// B packed as (column, value) records for the numeric tile pass: one load brings both.
-template <typename T> struct BRec { int32_t c; int32_t pad; T v; };   // complex: 16 / 24 B
-template <> struct __attribute__((aligned(16))) BRec<double> { int32_t c; int32_t pad; double v; };
-template <> struct __attribute__((aligned(8))) BRec<float> { int32_t c; float v; };
+// Tile-major B records: the entry's column inside its tile (32 bits) followed by its value,
+// packed without padding -- 8 bytes (f32), 12 bytes (f64, complex64), 20 bytes
+// (complex128) -- so one dwordx2 / dwordx3 load brings both, and the slice of a tile the
+// XCD keeps in L2 is as small as the values allow.  Offsets are 32-bit byte offsets from
+// the (scalar) base: the host keeps the record array under 4 GiB on the tile path.
+template <typename T> constexpr int rec_words() { return 1 + (int)(sizeof(T) / 4); }
 
-// One load per record: 16 bytes (f64) or 8 bytes (f32).
 template <typename T, typename IP>
-__device__ __forceinline__ void load_rec(const BRec<T>* __restrict__ rec, IP i, int& c, T& v) {
-    if constexpr (!std::is_same<T, double>::value && !std::is_same<T, float>::value) {
-        c = rec[i].c;
-        v = rec[i].v;
-    } else if constexpr (sizeof(T) == 8) {
-        const uint4 q = reinterpret_cast<const uint4*>(rec)[i];
-        c = (int)q.x;
-        v = __hiloint2double((int)q.w, (int)q.z);
-    } else {
-        const uint2 q = reinterpret_cast<const uint2*>(rec)[i];
-        c = (int)q.x;
-        v = __uint_as_float(q.y);
+__device__ __forceinline__ void load_rec(const uint32_t* __restrict__ rec, IP i, int& lc, T& v) {
+    constexpr int W = rec_words<T>();
+    const uint32_t* __restrict__ q =
+        reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(rec) + (uint64_t)((uint32_t)i * (uint32_t)(4 * W)));
+    if constexpr (W == 2) {          // f32
+        const uint2 x = *reinterpret_cast<const uint2*>(q);
+        lc = (int)x.x;
+        v = __uint_as_float(x.y);
+    } else if constexpr (W == 3) {   // f64, complex64
+        const uint3 x = *reinterpret_cast<const uint3*>(q);
+        lc = (int)x.x;
+        if constexpr (std::is_same<T, double>::value) {
+            v = __hiloint2double((int)x.z, (int)x.y);
+        } else {
+            v.re = __uint_as_float(x.y);
+            v.im = __uint_as_float(x.z);
+        }
+    } else {                          // complex128
+        lc = (int)q[0];
+        __builtin_memcpy(&v, q + 1, sizeof(T));
     }
 }
 
 template <typename T>
-__global__ __launch_bounds__(256) void k_pack_b(int64_t nnz, const int32_t* __restrict__ Bj,
-                                                const T* __restrict__ Bx, BRec<T>* __restrict__ rec) {
-    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < nnz; e += (int64_t)gridDim.x * 256) {
-        BRec<T> r;
-        r.c = Bj[e];
-        if constexpr (!std::is_same<T, float>::value) r.pad = 0;
-        r.v = Bx[e];
-        rec[e] = r;
+__device__ __forceinline__ void store_rec(uint32_t* __restrict__ rec, int64_t i, int lc, T v) {
+    constexpr int W = rec_words<T>();
+    uint32_t* q = rec + i * W;
+    q[0] = (uint32_t)lc;
+    __builtin_memcpy(q + 1, &v, sizeof(T));
+}
+
+// ---------------------------------------------------------------------------------------
+// Tile-major B.  For every numeric tile g, B's entries with columns in g, row by row: a CSR
+// of B's column slice g, the slices one after another.  tptr[g*(K+1) + k] is the offset of
+// row k's segment of tile g in the record array and tptr[g*(K+1) + K] the start of tile g+1,
+// so a (row, tile) item finds each A entry's segment with two adjacent 4-byte loads from a
+// K-entry table, and the items of one tile read one contiguous slice of B (an XCD working
+// through a tile keeps that slice and its table in its L2).  Built once per plan from the
+// row-major boundary index (k_tile_index, a temporary):
+//   k_bt_count   segment lengths into tptr (tile-major) and symbolic-tile starts into sidx
+//   k_scan_lb    lengths -> offsets, in place
+//   k_bt_pack    every B entry to its place (column, value record)
+__global__ __launch_bounds__(256) void k_bt_count(int64_t K, int G, int R, const uint2* __restrict__ tidx,
+                                                  int32_t* __restrict__ tptr, uint32_t* __restrict__ sidx) {
+    const int64_t n = K * G;
+    const int Gs = (G + R - 1) / R;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n + G; i += (int64_t)gridDim.x * 256) {
+        if (i >= n) {   // the end slot of each tile
+            tptr[(i - n) * (K + 1) + K] = 0;
+            continue;
+        }
+        const int64_t k = i / G;
+        const int g = (int)(i - k * G);
+        const uint2 se = tidx[i];
+        tptr[(int64_t)g * (K + 1) + k] = (int32_t)(se.y - se.x);
+        if (g % R == 0) sidx[k * (Gs + 1) + g / R] = se.x;
+        if (g == G - 1) sidx[k * (Gs + 1) + Gs] = se.y;
     }
+}
+
+// One wave per B row: an entry's rank inside its tile segment is its distance to the
+// segment's first entry, found by a max-scan over the lanes where the tile id steps.
+template <typename T, typename IP>
+__global__ __launch_bounds__(256) void k_bt_pack(int64_t K, const IP* __restrict__ Bp, const int32_t* __restrict__ Bj,
+                                                 const T* __restrict__ Bx, int tws,
+                                                 const int32_t* __restrict__ tptr, uint32_t* __restrict__ rec) {
+    const int l = lane_id();
+    const int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (k >= K) return;
+    const IP r0 = Bp[k];
+    const int len = (int)(Bp[k + 1] - r0);
+    int carry = 0;   // first entry of the segment the previous chunk ended in
+    for (int e0 = 0; e0 < len; e0 += WAVE) {
+        const int e = e0 + l;
+        const bool in = e < len;
+        const int32_t c = in ? Bj[r0 + e] : 0;
+        const int g = c >> tws;
+        int gp = __shfl_up(g, 1, WAVE);
+        if (l == 0) gp = e0 == 0 ? -1 : (Bj[r0 + e0 - 1] >> tws);
+        const int s0 = max(wave_incl_max_dpp((in && g != gp) ? e : -1), carry);
+        carry = readlane_i(s0, WAVE - 1);
+        if (in) store_rec(rec, (int64_t)tptr[(int64_t)g * (K + 1) + k] + (e - s0), c & ((1 << tws) - 1), Bx[r0 + e]);
+    }
+}
+
+// (start, end) of B row k's segment in a tile: two adjacent table words with one 8-byte
+// load (4-byte aligned: one request instead of two)
+__device__ __forceinline__ uint2 seg_pair(const int32_t* __restrict__ tp, int32_t k) {
+    uint2 v;
+    __builtin_memcpy(&v, tp + k, sizeof(v));
+    return v;
 }
 
 // Blocks are dispatched round-robin over the 8 XCDs.  Logical block ids that keep
@@ -126,69 +193,66 @@ template <typename IP> struct SymLds {
     uint32_t bits[SYM_NWMAX];
     IP jb0[WAVE];
     uint32_t joff[WAVE];
-    int8_t mk[TILE_MK];
+    uint8_t mk[TILE_MK];
 };
 
 // Lane -> A-entry map for a group of up to 16 chunks (1024 products) starting at gbase.
+// Marker byte l + 1 where A entry l's products start, 0 elsewhere, stored transposed: the
+// marker of product t (group-relative) at byte 16 * (t % 64) + t / 64, so each lane reads
+// the markers of all 16 chunks of its lane position with one 16-byte LDS load.  An
+// unsigned max-scan over a chunk's 64 markers (identity 0: one v_max_u32_dpp per step)
+// gives each lane its A entry + 1; `carry` (0 = none yet) brings it over from the previous
+// chunk.
 template <typename L>
 __device__ __forceinline__ void group_markers(L& S, int l, int cnt, int off, int gbase) {
     wsync();
-    reinterpret_cast<uint4*>(S.mk)[l] = make_uint4(~0u, ~0u, ~0u, ~0u);
+    reinterpret_cast<uint4*>(S.mk)[l] = make_uint4(0u, 0u, 0u, 0u);
     wsync();
-    if (cnt > 0 && off >= gbase && off < gbase + TILE_MK) S.mk[off - gbase] = (int8_t)l;
+    if (cnt > 0 && off >= gbase && off < gbase + TILE_MK) {
+        const int t = off - gbase;
+        S.mk[((t & (WAVE - 1)) << 4) | (t >> 6)] = (uint8_t)(l + 1);
+    }
     wsync();
 }
 
+// The marker bytes of chunks cb .. cb+7 of this lane's 16 (cb a multiple of the chunks per
+// step: 4 or 8), byte u = chunk cb + u.
+__device__ __forceinline__ uint64_t marker_bytes(uint4 m, int cb) {
+    const uint64_t lo = ((uint64_t)m.y << 32) | m.x, hi = ((uint64_t)m.w << 32) | m.z;
+    if (cb == 0) return lo;
+    if (cb >= 8) return hi >> (8 * (cb - 8));
+    return (lo >> (8 * cb)) | (hi << (64 - 8 * cb));
+}
+
 // Chunks of one group (<= 16 x 64 products) U at a time: map lanes to A entries for U
-// chunks, issue all their B loads, then hand each chunk to `fn(col, bval, aval)` in order
-// (lanes past the group's products get col = -1).
-template <int U, bool VALS, typename T, typename IP, typename L, typename F>
-__device__ __forceinline__ void walk_group(L& S, int l, int gb, int Pb, int& carry,
-                                           const int32_t* __restrict__ Bj,
-                                           const T* __restrict__ Bx, F&& fn,
-                                           const BRec<T>* __restrict__ rec = nullptr) {
+// chunks, issue all their column loads, then hand each chunk to `fn(col)` in order (lanes
+// past the group's products get col = -1).
+template <int U, typename IP, typename L, typename F>
+__device__ __forceinline__ void walk_group(L& S, int l, int gb, int Pb, unsigned& carry,
+                                           const int32_t* __restrict__ Bj, F&& fn) {
     const int nchg = min(TILE_MK, Pb - gb);
+    const uint4 mrow = reinterpret_cast<const uint4*>(S.mk)[l];
     for (int c0 = 0; c0 < nchg; c0 += U * WAVE) {
+        const uint64_t mb = marker_bytes(mrow, c0 >> 6);
         IP idx[U];
-        T av[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             idx[u] = (IP)-1;
-            av[u] = (T)0;
             const int cc = c0 + u * WAVE;
             if (cc < nchg) {
-                const int src = max(wave_incl_max_dpp((int)S.mk[cc + l]), carry);
-                carry = readlane_i(src, WAVE - 1);
+                const unsigned sp = max(wave_incl_umax_dpp((unsigned)(mb >> (8 * u)) & 0xffu), carry);
+                carry = (unsigned)readlane_i((int)sp, WAVE - 1);
+                const int src = (int)sp - 1;
                 const int t = gb + cc + l;
-                if (t < Pb) {
-                    idx[u] = S.jb0[src] + (IP)(t - (int)S.joff[src]);
-                    if constexpr (VALS) av[u] = S.ja[src];
-                }
+                if (t < Pb) idx[u] = S.jb0[src] + (IP)(t - (int)S.joff[src]);
             }
         }
         int col[U];
-        T bv[U];
-        if (VALS && rec) {
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                col[u] = -1;
-                bv[u] = (T)0;
-                if (idx[u] >= 0) {
-                    const BRec<T> r = rec[idx[u]];
-                    col[u] = r.c;
-                    bv[u] = r.v;
-                }
-            }
-        } else {
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                col[u] = idx[u] >= 0 ? Bj[idx[u]] : -1;
-                bv[u] = (VALS && idx[u] >= 0) ? Bx[idx[u]] : (T)0;
-            }
-        }
+        for (int u = 0; u < U; ++u) col[u] = idx[u] >= 0 ? Bj[idx[u]] : -1;
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            if (c0 + u * WAVE < nchg) fn(col[u], bv[u], av[u]);
+            if (c0 + u * WAVE < nchg) fn(col[u]);
     }
 }
 
@@ -200,7 +264,7 @@ template <typename IP>
 __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile_sym(
     int64_t row0, int64_t nrows, int tws, int G, int twss, const IP* __restrict__ Ap,
     const int32_t* __restrict__ Aj, const IP* __restrict__ Bp, const int32_t* __restrict__ Bj,
-    const uint2* __restrict__ tidx, uint32_t* __restrict__ bitmap, int64_t* __restrict__ item_cnt) {
+    const uint32_t* __restrict__ sidx, uint32_t* __restrict__ bitmap, int64_t* __restrict__ item_cnt) {
     __shared__ __attribute__((aligned(16))) SymLds<IP> lds[TILE_WPB];
     const int l = lane_id();
     const int wv = uniform((int)(threadIdx.x >> 6));
@@ -219,7 +283,7 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile_sym(
         const int64_t a0 = Ap[row];
         const int nA = (int)(Ap[row + 1] - a0);
         if (nA <= 0) {
-            for (int t = t0 + l; t < t1; t += WAVE) item_cnt[row * G + t] = 0;
+            for (int t = t0 + l; t < t1; t += WAVE) item_cnt[(row - row0) * G + t] = 0;
             continue;
         }
         wsync();
@@ -234,9 +298,9 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile_sym(
                     cnt = (int)(Bp[k + 1] - rb);
                     beg = rb;
                 } else {
-                    const uint2* tk = tidx + (int64_t)k * G;
-                    const uint32_t s0 = tk[t0].x;
-                    cnt = (int)(tk[t1 - 1].y - s0);
+                    const uint32_t* sk = sidx + (int64_t)k * (Gs + 1);
+                    const uint32_t s0 = sk[gs];
+                    cnt = (int)(sk[gs + 1] - s0);
                     beg = rb + (IP)s0;
                 }
             }
@@ -247,41 +311,54 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile_sym(
             S.jb0[l] = beg;
             S.joff[l] = (uint32_t)off;
             wsync();
-            int carry = -1;
+            unsigned carry = 0u;
             for (int gb = 0; gb < Pb; gb += TILE_MK) {
                 group_markers(S, l, cnt, off, gb);
-                walk_group<8, false, float, IP>(S, l, gb, Pb, carry, Bj, (const float*)nullptr,
-                                               [&](int c, float, float) {
-                                                   if (c >= 0) set_bit(S.bits, c - lo);
-                                               });
+                walk_group<8, IP>(S, l, gb, Pb, carry, Bj, [&](int c) {
+                    if (c >= 0) set_bit(S.bits, c - lo);
+                });
             }
         }
         wsync();
-        uint32_t* __restrict__ out = bitmap + (row * G + t0) * (int64_t)nw;
+        uint32_t* __restrict__ out = bitmap + ((row - row0) * G + t0) * (int64_t)nw;
         for (int w = l; w < nws; w += WAVE) out[w] = S.bits[w];
         // entry count of each numeric tile: lane t sums tile t's words (rotated start: no
         // two lanes read one bank together)
         for (int t = l; t < t1 - t0; t += WAVE) {
             int c = 0;
             for (int j = 0; j < nw; ++j) c += __popc(S.bits[t * nw + ((j + t) & (nw - 1))]);
-            item_cnt[row * G + t0 + t] = c;
+            item_cnt[(row - row0) * G + t0 + t] = c;
         }
     }
 }
 
 // Numeric pass of the tile path: one wave per item (row, numeric tile).  Reads the item's
 // bitmap from the symbolic pass, enumerates its products in flattened (jj, kk) order --
-// one 8-byte index load per A entry, one record load per product from the packed B --
-// and accumulates lowest-lane-first per output position; items with more than CAP entries
-// go in column windows (products re-read per window).
-template <typename T, typename IP>
+// two adjacent 4-byte loads from tile g's segment table per A entry, one record load per
+// product from tile g's slice of the tile-major B -- and accumulates lowest-lane-first per
+// output position.  Items are taken tile-major (item = g * nrows + row) and the XCD-aware
+// block map gives every XCD a contiguous run of them: an XCD works through one tile at a
+// time, so the tile's B slice and segment table stay in its L2, while the eight XCDs sweep
+// the A rows in the same order (an A row comes from HBM about once per eight tiles, the
+// other reads hit the Infinity Cache).
+//
+// Positions: DENSE (tile width <= CAP, one window) addresses the accumulator by column
+// (c - lo); otherwise by the popcount prefix of the symbolic bitmap, in column windows of
+// <= CAP entries (products re-read per window).
+// Ordered adds: products are taken U chunks (U * 64) at a time, all their record loads in
+// flight; then groups of RU chunks resolve collisions in owner rounds: a ds_min of the key
+// (round, chunk, lane) per product, the product whose key stuck adds, the others retry with
+// the next (smaller) round number.  Within a group the lowest (chunk, lane) -- the earliest
+// product in flattened order -- of every position adds first; groups run in order.
+template <typename T, typename IP, bool DENSE, int RU>
 __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile(
     int64_t row0, int64_t nrows, int tws, int G, const IP* __restrict__ Ap,
-    const int32_t* __restrict__ Aj, const T* __restrict__ Ax, const IP* __restrict__ Bp,
-    const BRec<T>* __restrict__ brec, const uint2* __restrict__ tidx,
+    const int32_t* __restrict__ Aj, const T* __restrict__ Ax, int64_t K,
+    const uint32_t* __restrict__ brec, const int32_t* __restrict__ tptr,
     const uint32_t* __restrict__ bitmap, const int64_t* __restrict__ item_off,
-    int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha) {
+    int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha, int diag) {
     constexpr int U = sizeof(T) > 8 ? 4 : 8;   // chunks in flight (complex128: half)
+    static_assert(U % RU == 0, "round groups split the chunks in flight");
     __shared__ __attribute__((aligned(16))) NumLds<T, IP> lds[TILE_WPB];
     const int l = lane_id();
     const int wv = uniform((int)(threadIdx.x >> 6));
@@ -291,9 +368,10 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile(
     const int wpl = (nw + WAVE - 1) / WAVE;    // words per lane (<= 2)
     const uint32_t items = (uint32_t)(nrows * G);   // host keeps rows*G < 2^31
     for (uint32_t it = xcd_block(gridDim.x) * TILE_WPB + wv; it < items; it += gridDim.x * TILE_WPB) {
-        const int64_t row = row0 + (int64_t)(it / (uint32_t)G);
-        const int g = (int)(it % (uint32_t)G);
-        const int64_t item = row * G + g;
+        const int g = (int)(it / (uint32_t)nrows);
+        const int64_t row = row0 + (int64_t)(it - (uint32_t)g * (uint32_t)nrows);
+        const int64_t item = (row - row0) * G + g;   // items (and bitmaps) of this chunk of rows
+        const int32_t* __restrict__ tp = tptr + (int64_t)g * (K + 1);   // tile g's segment table
         const int lo = g * TW;
         const int64_t a0 = Ap[row];
         const int nA = (int)(Ap[row + 1] - a0);
@@ -326,13 +404,12 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile(
         wsync();
         const int64_t obase = item_off[item];
         // The first NB batches of A entries (rows of <= NB*64 entries: all of them): every
-        // lane's A entry, value, tile segment and B row start, loaded at once up front (two
-        // dependent load levels per item instead of two per batch).
+        // lane's A entry, value and tile segment, loaded at once up front (two dependent
+        // load levels per item instead of two per batch).
         constexpr int NB = sizeof(T) > 8 ? 4 : 8;
         int32_t kq[NB];
         T aq[NB];
         uint2 sq[NB];
-        IP bq[NB];
 #pragma unroll
         for (int q = 0; q < NB; ++q) {
             kq[q] = -1;
@@ -345,11 +422,7 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile(
 #pragma unroll
         for (int q = 0; q < NB; ++q) {
             sq[q] = make_uint2(0u, 0u);
-            bq[q] = 0;
-            if (kq[q] >= 0) {
-                sq[q] = tidx[(int64_t)kq[q] * G + g];
-                bq[q] = Bp[kq[q]];
-            }
+            if (kq[q] >= 0) sq[q] = seg_pair(tp, kq[q]);
         }
         // lane info of one batch of A entries: (first B index, count) of its tile segment
         auto batch = [&](int b, int& cnt, int& off, int& Pb) {
@@ -361,14 +434,13 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile(
                 for (int q = 0; q < NB; ++q)
                     if (q == (b >> 6)) {
                         cnt = (int)(sq[q].y - sq[q].x);
-                        beg = bq[q] + (IP)sq[q].x;
+                        beg = (IP)sq[q].x;
                         av = aq[q];
                     }
             } else if (b + l < nA) {
-                const int32_t k = Aj[a0 + b + l];
-                const uint2 se = tidx[(int64_t)k * G + g];
+                const uint2 se = seg_pair(tp, Aj[a0 + b + l]);
                 cnt = (int)(se.y - se.x);
-                beg = Bp[k] + (IP)se.x;
+                beg = (IP)se.x;
                 av = Ax[a0 + b + l];
             }
             const int incl = wave_incl_sum_dpp(cnt);
@@ -380,85 +452,123 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile(
         };
         for (int L0 = 0; L0 < WAVE;) {
             int L1 = WAVE, wb = 0, wn = nnz;
-            if (nnz > TILE_CAP) {
+            if (!DENSE && nnz > TILE_CAP) {
                 wb = readlane_i(p0, L0);
                 L1 = (int)__popcll(__ballot(pincl <= wb + TILE_CAP));
                 if (L1 <= L0) L1 = L0 + 1;
                 wn = (L1 < WAVE ? readlane_i(p0, L1) : nnz) - wb;
             }
-            const int clo = lo + 32 * wpl * L0, chi = lo + 32 * wpl * L1;
-            for (int p = l; p < wn; p += WAVE) {
-                S.acc[p] = (T)0;
-                S.tag[p] = 0xffffffffu;
+            const int clo = 32 * wpl * L0, chi = 32 * wpl * L1;   // window, tile-relative
+            const int span = DENSE ? TW : wn;   // accumulator slots in use
+            if constexpr (DENSE) {   // 16-byte stores (TW is a multiple of 64)
+                uint4* a4 = reinterpret_cast<uint4*>(S.acc);
+                uint4* t4 = reinterpret_cast<uint4*>(S.tag);
+                for (int q = l; q < TW * (int)sizeof(T) / 16; q += WAVE) a4[q] = make_uint4(0u, 0u, 0u, 0u);
+                for (int q = l; q < TW / 4; q += WAVE) t4[q] = make_uint4(~0u, ~0u, ~0u, ~0u);
+            } else {
+                for (int p = l; p < span; p += WAVE) {
+                    S.acc[p] = (T)0;
+                    S.tag[p] = 0xffffffffu;
+                }
             }
             wsync();
             uint32_t seq = 0x7fffffu;   // 23 bits: key = seq | chunk (3 bits) | lane (6 bits)
-            for (int b = 0; b < nA; b += WAVE) {
+            for (int b = 0; b < ((diag & 4) ? 0 : nA); b += WAVE) {   // (diag 4, timing only: no batches)
                 int cnt, off, Pb;
                 batch(b, cnt, off, Pb);
-                int carry = -1;
+                unsigned carry = 0u;
                 for (int gb = 0; gb < Pb; gb += TILE_MK) {
                     group_markers(S, l, cnt, off, gb);
                     const int nchg = min(TILE_MK, Pb - gb);
+                    const uint4 mrow = reinterpret_cast<const uint4*>(S.mk)[l];
                     for (int c0 = 0; c0 < nchg; c0 += U * WAVE) {
-                        // lane -> A entry of U chunks at once; chunks past the group read the
-                        // -1 markers, so `carry` passes through them unchanged.  Indices of
-                        // lanes past the group are clamped to 0 and their results dropped.
-                        IP idx[U];
-                        T av[U];
-                        bool val[U];
+                        // U chunks at once, or U/2 when no more hold products (a wave-uniform
+                        // choice: no empty slots scanned and loaded for short batches)
+                        const int nu = min(U, (nchg - c0 + WAVE - 1) >> 6);
+                        auto step = [&](auto nuc) {
+                            constexpr int NU = decltype(nuc)::value;
+                            constexpr int RG = RU < NU ? RU : NU;
+                            // NU chunks at once (nu of them hold products: a wave-uniform count):
+                            // the lane -> A entry scans, then every record load in flight.
+                            const uint64_t mb = marker_bytes(mrow, c0 >> 6);
+                            // (slots past nu scan zero markers and load record 0: no branches
+                            // between the loads, so they all stay in flight)
+                            unsigned sp[NU];
 #pragma unroll
-                        for (int u = 0; u < U; ++u) {
-                            const int cc = c0 + u * WAVE;
-                            const int src = max(wave_incl_max_dpp((int)S.mk[cc + l]), carry);
-                            carry = readlane_i(src, WAVE - 1);
-                            const int t = gb + cc + l;
-                            val[u] = t < Pb;
-                            const TileEnt<T, IP> e = S.ent[max(src, 0)];
-                            idx[u] = val[u] ? e.jb0 + (IP)(t - (int)e.joff) : (IP)0;
-                            av[u] = e.ja;
-                        }
-                        int qc[U];
-                        T qv[U];
+                            for (int u = 0; u < NU; ++u) sp[u] = wave_incl_umax_dpp((unsigned)(mb >> (8 * u)) & 0xffu);
 #pragma unroll
-                        for (int u = 0; u < U; ++u) load_rec(brec, idx[u], qc[u], qv[u]);
-                        // positions and products of all U chunks, then one joint owner
-                        // round for the U*64 products: key (seq, chunk, lane) orders them by
-                        // flattened index, so the lowest pending product of every position
-                        // adds first; a lane's U atomics are independent and pipeline
-                        int pos[U];
-                        T pv[U];
-                        uint32_t pend = 0u;
-#pragma unroll
-                        for (int u = 0; u < U; ++u) {
-                            const int c = (val[u] && c0 + u * WAVE < nchg) ? qc[u] : -1;
-                            pos[u] = 0;
-                            if (c >= clo && c < chi) {
-                                const int rc = c - lo;
-                                const uint2 bw = S.bw[rc >> 5];
-                                pos[u] = (int)bw.y + __popc(bw.x & ((1u << (rc & 31)) - 1u)) - wb;
-                                pend |= 1u << u;
+                            for (int u = 0; u < NU; ++u) {
+                                sp[u] = max(sp[u], carry);
+                                carry = (unsigned)readlane_i((int)sp[u], WAVE - 1);
                             }
-                            pv[u] = mul_rn(av[u], qv[u]);
-                        }
-                        while (__ballot(pend != 0u)) {
-                            const uint32_t kb = (seq << 9) | (uint32_t)l;
+                            IP idx[NU];
+                            T av[NU];
+                            bool val[NU];
 #pragma unroll
-                            for (int u = 0; u < U; ++u)
-                                if (pend & (1u << u)) atomicMin(&S.tag[pos[u]], kb | ((uint32_t)u << 6));
+                            for (int u = 0; u < NU; ++u) {
+                                const int t = gb + c0 + u * WAVE + l;
+                                val[u] = u < nu && t < Pb;
+                                const TileEnt<T, IP> e = S.ent[(int)max(sp[u], 1u) - 1];
+                                idx[u] = val[u] ? e.jb0 + (IP)(t - (int)e.joff) : (IP)0;
+                                av[u] = e.ja;
+                            }
+                            int qc[NU];
+                            T qv[NU];
+                            if (diag & 2) {   // timing only: no record loads
 #pragma unroll
-                            for (int u = 0; u < U; ++u)
-                                if ((pend & (1u << u)) &&
-                                    __hip_atomic_load(&S.tag[pos[u]], __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_WAVEFRONT) == (kb | ((uint32_t)u << 6))) {
-                                    S.acc[pos[u]] = add_rn(S.acc[pos[u]], pv[u]);
-                                    pend &= ~(1u << u);
+                                for (int u = 0; u < NU; ++u) { qc[u] = (int)((idx[u] * 37u) & (uint32_t)(TW - 1)); qv[u] = (T)1; }
+                            } else {
+#pragma unroll
+                                for (int u = 0; u < NU; ++u) load_rec(brec, idx[u], qc[u], qv[u]);
+                            }
+                            int pos[NU];
+                            T pv[NU];
+                            uint32_t pend = 0u;
+#pragma unroll
+                            for (int u = 0; u < NU; ++u) {
+                                pos[u] = 0;
+                                pv[u] = (T)0;
+                                {
+                                    const int rc = val[u] ? qc[u] : -1;   // column inside the tile
+                                    if constexpr (DENSE) {
+                                        if (rc >= 0) {
+                                            pos[u] = rc;
+                                            pend |= 1u << u;
+                                        }
+                                    } else if (rc >= clo && rc < chi) {
+                                        const uint2 bw = S.bw[rc >> 5];
+                                        pos[u] = (int)bw.y + __popc(bw.x & ((1u << (rc & 31)) - 1u)) - wb;
+                                        pend |= 1u << u;
+                                    }
+                                    pv[u] = mul_rn(av[u], qv[u]);
                                 }
-                            --seq;
-                        }
+                            }
+                            if (diag & 1) pend = 0u;   // timing only: no accumulation
+#pragma unroll
+                            for (int u0 = 0; u0 < NU; u0 += RG) {
+                                uint32_t gm = pend & (((1u << RG) - 1u) << u0);
+                                while (__ballot(gm != 0u)) {
+                                    const uint32_t kb = (seq << 9) | (uint32_t)l;
+#pragma unroll
+                                    for (int u = u0; u < u0 + RG; ++u)
+                                        if (gm & (1u << u)) atomicMin(&S.tag[pos[u]], kb | ((uint32_t)u << 6));
+#pragma unroll
+                                    for (int u = u0; u < u0 + RG; ++u)
+                                        if ((gm & (1u << u)) &&
+                                            __hip_atomic_load(&S.tag[pos[u]], __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_WAVEFRONT) == (kb | ((uint32_t)u << 6))) {
+                                            S.acc[pos[u]] = add_rn(S.acc[pos[u]], pv[u]);
+                                            gm &= ~(1u << u);
+                                        }
+                                    --seq;
+                                }
+                            }
+                        };
+                        if (nu > U / 2) step(std::integral_constant<int, U>{});
+                        else step(std::integral_constant<int, U / 2>{});
                         if (seq < 4096u) {   // re-arm the tag space (very long items only)
                             wsync();
-                            for (int p = l; p < wn; p += WAVE) S.tag[p] = 0xffffffffu;
+                            for (int p = l; p < span; p += WAVE) S.tag[p] = 0xffffffffu;
                             seq = 0x7fffffu;
                             wsync();
                         }
@@ -466,6 +576,27 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile(
                 }
             }
             wsync();
+            if constexpr (DENSE) {
+                // every set bit of the tile's bitmap, in column order: lane l looks at bit
+                // l % 32 of word 2i + l / 32; its output position is the word's prefix plus
+                // the bits below it
+                int32_t* __restrict__ crow = Cj + obase;
+                T* __restrict__ xrow = Cx + obase;
+                for (int wq = 0; wq < nw; wq += 2) {
+                    const int w = wq + (l >> 5), bt = l & 31;
+                    if (w < nw) {
+                        const uint2 bw = S.bw[w];
+                        if (((bw.x >> bt) & 1u) && !(diag & 8)) {   // (diag 8, timing only: no output)
+                            const int p = (int)bw.y + __popc(bw.x & ((1u << bt) - 1u));
+                            crow[p] = lo + 32 * w + bt;
+                            const T val = S.acc[32 * w + bt];
+                            xrow[p] = (alpha == (T)1) ? val : mul_rn(alpha, val);
+                        }
+                    }
+                }
+                wsync();
+                break;
+            }
             // column list of this window from the bitmap (lane-owned words)
             if (l >= L0 && l < L1) {
                 int p = p0 - wb;
@@ -481,7 +612,8 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile(
             int32_t* __restrict__ crow = Cj + obase + wb;
             T* __restrict__ xrow = Cx + obase + wb;
             for (int p = l; p < wn; p += WAVE) {
-                crow[p] = (int32_t)S.tag[p];
+                const uint32_t c = S.tag[p];
+                crow[p] = (int32_t)c;
                 const T val = S.acc[p];
                 xrow[p] = (alpha == (T)1) ? val : mul_rn(alpha, val);
             }

@@ -170,7 +170,10 @@ def spgemm(a, b, alpha=1, alg=0, chunk_fraction=0.2, verbose=False):
     nnz, peak = ctypes.c_int64(0), ctypes.c_size_t(0)
     pj, px, plan = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
     # plan -> symbolic (nnz(C) to the host) -> numeric in one call (spg_spgemm_ws)
-    for it in (torch.int32, torch.int64):   # int64 row pointer once nnz(C) >= 2**31
+    # int64 row pointer once nnz(C) >= 2**31; int64 first when the expected product count
+    # reaches 2**31 (an overflowing int32 try would redo the plan and the symbolic pass)
+    wide = a.nnz * (b.nnz / max(b.shape[0], 1)) >= 2 ** 31
+    for it in ((torch.int64,) if wide else (torch.int32, torch.int64)):
         indptr = torch.empty(m + 1, dtype=it, device=dev)
         st = lib.spg_spgemm_ws(h.ptr, ctypes.byref(va), ctypes.byref(vb), algo, cf, ctypes.byref(al),
                                ctypes.c_void_p(ws.data_ptr()), ws_bytes.value,
@@ -195,6 +198,8 @@ def spgemm(a, b, alpha=1, alg=0, chunk_fraction=0.2, verbose=False):
             check(lib.spg_numeric(h.ptr, plan, ctypes.byref(al), ctypes.byref(vc)), "spg_numeric")
         finally:
             lib.spg_plan_destroy(plan)
+    if wide and nnzc < 2 ** 31:
+        indptr = indptr.to(torch.int32)   # the int32 contract when the result fits
     last_stats.alg, last_stats.workspace_bytes = int(algo), int(ws_bytes.value)
     last_stats.peak_bytes, last_stats.nnz = int(peak.value), nnzc
     return csr_matrix._from_parts(data, indices, indptr, (m, n), canonical=True)

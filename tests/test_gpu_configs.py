@@ -1,0 +1,155 @@
+"""BASELINE.json's GPU configurations at their full sizes, through the C ABI.
+
+* Config 3 (dense_vs_sparseGEMM sweep, N = 8192): the upper half of the sweep in full,
+  density 1e-2 and 1e-1 (ALG2), bit-exact against the CPU oracle over every row (the OpenMP
+  oracle for 1e-1: 5.5e9 products).
+* Config 4 (N = 65536, density 5e-3, ALG3 chunked): nnz(C) = 3.46e9 needs an int64 row
+  pointer.  256 sampled rows bit-exact against the oracle, plus size-independent properties
+  over the whole result: int64 row pointer, monotone, row_ptr[-1] = nnz(C) within the
+  analytic expectation, every row's columns strictly increasing and in range, no row longer
+  than its product count or N, and P (getNumProducts) equal to sum over A's entries of the
+  B row lengths.
+* Config 5 on one GPU (N = 262144, density 1e-3, ALG2): the same checks (200 GB of C and
+  workspace fit the 288 GB of one MI355X).
+* ALG3's working-set cap on a tile-path shape: peak bytes fall as chunk_fraction falls,
+  with bit-identical results.
+
+Inputs of configs 4/5 are generated on the device (spmm_amd.gen.random_csr); the oracle
+sees only the sampled rows of A (and all of B).
+"""
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from oracle import oracle
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+THREADS = 16   # the GPU box's CPU share
+
+
+def _bits(x):
+    return x.view(np.uint32 if x.dtype == np.float32 else np.uint64)
+
+
+def _full_bitexact(Ah, Bh, alg, cf=0.2, threads=0):
+    from spmm_amd import cusparse
+    from spmm_amd.sparse import csr_matrix
+    C = cusparse.spgemm(csr_matrix(Ah, device=DEV), csr_matrix(Bh, device=DEV), alg=alg, chunk_fraction=cf)
+    torch.cuda.synchronize()
+    rp, rj, rx = oracle.spgemm(Ah, Bh, keep_zeros=True, sort=True, threads=threads)
+    assert np.array_equal(C.indptr.cpu().numpy().astype(np.int64), rp), "row pointer"
+    assert np.array_equal(C.indices.cpu().numpy(), rj), "column indices"
+    assert np.array_equal(_bits(C.data.cpu().numpy()), _bits(rx)), "values"
+    return C
+
+
+@pytest.mark.parametrize("density", [1e-2, 1e-1])
+def test_config3_full_bitexact(density):
+    from spmm_amd import gen
+    Ah, Bh = gen.scipy_pair(8192, density, seed=42)
+    C = _full_bitexact(Ah, Bh, alg=2, threads=THREADS if density >= 0.1 else 0)
+    if density >= 0.1:
+        assert C.nnz == 8192 * 8192   # every entry of C is reached at density 0.1
+
+
+def _expected_nnz(a_lens, n, density):
+    """E[nnz(C)] for B with independent uniform columns: sum_i n (1 - (1 - d)^{a_i})."""
+    a = a_lens.astype(np.float64)
+    return float(np.sum(n * (1.0 - np.power(1.0 - density, a))))
+
+
+@torch.no_grad()
+def _check_structure(A, B, C, n, density):
+    """Size-independent properties of C over every row (device-side, in row chunks)."""
+    m = A.shape[0]
+    p = C.indptr
+    assert p.dtype == torch.int64, "nnz(C) >= 2^31 needs an int64 row pointer"
+    assert int(p[0]) == 0 and int(p[-1]) == C.nnz
+    lens = p[1:] - p[:-1]
+    assert bool((lens >= 0).all()), "row pointer not monotone"
+    # P = sum over A's entries of B's row lengths; every row holds <= min(P_i, n) entries
+    blen = (B.indptr[1:] - B.indptr[:-1]).to(torch.int64)
+    prod = blen[A.indices.to(torch.int64)]
+    rows = torch.repeat_interleave(torch.arange(m, device=p.device),
+                                   (A.indptr[1:] - A.indptr[:-1]).to(torch.int64))
+    P_i = torch.zeros(m, dtype=torch.int64, device=p.device).index_add_(0, rows, prod)
+    assert bool((lens <= torch.clamp(P_i, max=n)).all())
+    # nnz(C) against its expectation (relative std ~1e-5 at these sizes)
+    exp = _expected_nnz((A.indptr[1:] - A.indptr[:-1]).cpu().numpy(), n, density)
+    assert abs(C.nnz - exp) / exp < 2e-3, (C.nnz, exp)
+    # columns in range and strictly increasing inside every row
+    step = max(1, int(4e8 // max(1, C.nnz // m)))   # ~4e8 entries per chunk
+    for r0 in range(0, m, step):
+        r1 = min(m, r0 + step)
+        s, e = int(p[r0]), int(p[r1])
+        if e <= s:
+            continue
+        cols = C.indices[s:e]
+        lo, hi = torch.aminmax(cols)
+        assert int(lo) >= 0 and int(hi) < n
+        start = torch.zeros(e - s, dtype=torch.bool, device=cols.device)
+        start[(p[r0:r1] - s)[lens[r0:r1] > 0]] = True
+        ok = (cols[1:] > cols[:-1]) | start[1:]
+        assert bool(ok.all()), f"columns not increasing in rows [{r0}, {r1})"
+        del cols, start, ok
+    return int(P_i.sum())
+
+
+def _sampled_bitexact(A, B, C, nrows, seed=0):
+    rng = np.random.default_rng(seed)
+    rows = np.sort(rng.choice(A.shape[0], size=nrows, replace=False))
+    Ah, Bh = A.get(), B.get()
+    rp, rj, rx = oracle.spgemm(sp.csr_matrix(Ah[rows]), Bh, keep_zeros=True, sort=True, threads=THREADS)
+    p = C.indptr.cpu().numpy()
+    for q, i in enumerate(rows):
+        s, e = int(p[i]), int(p[i + 1])
+        assert e - s == rp[q + 1] - rp[q], f"row {i}: nnz"
+        assert np.array_equal(C.indices[s:e].cpu().numpy(), rj[rp[q]:rp[q + 1]]), f"row {i}: columns"
+        assert np.array_equal(_bits(C.data[s:e].cpu().numpy()), _bits(rx[rp[q]:rp[q + 1]])), f"row {i}: values"
+
+
+@pytest.mark.parametrize("n,density,alg,cf,expect_products", [
+    (65536, 5e-3, 3, 0.2, 7.04e9),     # config 4
+    (262144, 1e-3, 2, 0.2, 1.80e10),   # config 5, one GPU
+])
+def test_large_config_sampled_and_properties(n, density, alg, cf, expect_products):
+    from spmm_amd import cusparse, gen
+    A = gen.random_csr(n, n, density, seed=42, device=DEV)
+    B = gen.random_csr(n, n, density, seed=43, device=DEV)
+    C = cusparse.spgemm(A, B, alg=alg, chunk_fraction=cf)
+    torch.cuda.synchronize()
+    P = _check_structure(A, B, C, n, density)
+    assert P == cusparse.num_products(A, B)
+    assert abs(P - expect_products) / expect_products < 0.02
+    _sampled_bitexact(A, B, C, 256)
+    del C
+    torch.cuda.empty_cache()
+
+
+def test_alg3_peak_falls_with_chunk_fraction():
+    """ALG3 caps the tile path's working set (items and bitmaps sized by the largest chunk,
+    reused chunk by chunk): peak bytes fall as chunk_fraction falls, the result does not
+    change (the reference's alg3.cu:195-202 / BASELINE.md 1a behaviour)."""
+    from spmm_amd import cusparse, gen
+    from spmm_amd.sparse import csr_matrix
+    Ah, Bh = gen.scipy_pair(8192, 1e-2, seed=42)
+    A, B = csr_matrix(Ah, device=DEV), csr_matrix(Bh, device=DEV)
+    peaks, ref = [], None
+    for cf in (1.0, 0.2, 0.05):
+        C = cusparse.spgemm(A, B, alg=3, chunk_fraction=cf)
+        torch.cuda.synchronize()
+        peaks.append(cusparse.last_stats.peak_bytes)
+        got = (C.indptr.cpu().numpy(), C.indices.cpu().numpy(), _bits(C.data.cpu().numpy()))
+        if ref is None:
+            ref = got
+        else:
+            assert all(np.array_equal(x, y) for x, y in zip(got, ref)), f"cf={cf} changed C"
+    assert peaks[0] > peaks[1] > peaks[2], peaks
+    # the workspace part (peak minus C's arrays) shrinks by at least 1.5x from cf=1 to
+    # cf=0.05 (what stays is the tile-major copy of B, independent of cf)
+    c_bytes = 12 * len(ref[1]) + 4 * len(ref[0])
+    assert (peaks[2] - c_bytes) * 1.5 <= (peaks[0] - c_bytes), (peaks, c_bytes)
