@@ -10,6 +10,10 @@ stay resident in the 256 MiB Infinity Cache it is an upper bound on HBM reads.  
 correction is calibrated for 16-B/lane streaming reads only: the gathers of B here are
 narrower, so the corrected read figure is an upper bound too (raw values are kept).
 
+Each entry is stamped with the build id of the library it was measured on
+(spmm_amd._lib.build_id(): SHA-256 of libmi355_spgemm.so); bench.py reports a traffic figure
+only when the stamp matches the library it runs.
+
 usage: pmc_to_json.py <dir> <key> <kernel regex> [json path]
 """
 import csv
@@ -18,6 +22,8 @@ import json
 import os
 import re
 import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 
 
 def per_launch(d, counter, rx):
@@ -36,6 +42,7 @@ def per_launch(d, counter, rx):
 
 
 def main():
+    from spmm_amd._lib import build_id
     d, key, pat = sys.argv[1], sys.argv[2], sys.argv[3]
     path = sys.argv[4] if len(sys.argv) > 4 else os.path.join(os.path.dirname(__file__), "pmc_traffic.json")
     rx = re.compile(pat)
@@ -50,7 +57,8 @@ def main():
                "fetch_size_kib": round(fetch, 1), "write_size_kib": round(write, 1),
                "read_bytes_per_launch": int(rd), "write_bytes_per_launch": int(wr),
                "hbm_bytes_per_launch": int(rd + wr),
-               "note": "FETCH_SIZE x2 (gfx950) + WRITE_SIZE; Infinity-Cache hits included"}
+               "note": "FETCH_SIZE x2 (gfx950) + WRITE_SIZE; Infinity-Cache hits included",
+               "build_id": build_id()}
     json.dump(db, open(path, "w"), indent=1, sort_keys=True)
     print(json.dumps({key: db[key]}))
 

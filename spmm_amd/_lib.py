@@ -122,6 +122,20 @@ def load():
     return _lib
 
 
+_build_id = None
+
+
+def build_id() -> str:
+    """First 16 hex digits of the SHA-256 of the library file in use: stamps measurements
+    (PMC traffic summaries) so a number collected on another build is not reused."""
+    global _build_id
+    if _build_id is None:
+        import hashlib
+        with open(LIB_PATH, "rb") as f:
+            _build_id = hashlib.sha256(f.read()).hexdigest()[:16]
+    return _build_id
+
+
 def check(status: int, where: str = "") -> None:
     if status != 0:
         raise SpgError(status, where)

@@ -36,6 +36,9 @@ spg_csr_t view(int64_t rows, int64_t cols, const at::Tensor& p, const at::Tensor
 std::tuple<int64_t, at::Tensor, at::Tensor, at::Tensor, int64_t, int64_t> spgemm(
     int64_t handle, int64_t m, int64_t k, int64_t n, at::Tensor Ap, at::Tensor Aj, at::Tensor Ax, at::Tensor Bp,
     at::Tensor Bj, at::Tensor Bx, int64_t alg, double chunk_fraction, double alpha_re, double alpha_im) {
+    // the library calls and allocations run without the GIL: other Python threads (the
+    // harness's free-memory sampler, profiling.profile_op_gpu) keep running during a product
+    pybind11::gil_scoped_release nogil;
     spg_handle_t h = reinterpret_cast<spg_handle_t>(handle);
     const spg_csr_t A = view(m, k, Ap, Aj, Ax), B = view(k, n, Bp, Bj, Bx);
     const spg_alg_t a = (spg_alg_t)alg;

@@ -214,6 +214,21 @@ inline int sym_tile_log2(const spg_csr_t& B, int tws) {
 }
 
 
+// Makes the handle's device current for one entry point and restores the caller's device
+// on exit (cuSPARSE leaves the current device alone; so does this library).
+struct DeviceGuard {
+    int prev = -1;
+    hipError_t err = hipSuccess;
+    explicit DeviceGuard(int dev) {
+        if ((err = hipGetDevice(&prev)) != hipSuccess) return;
+        if (prev != dev) err = hipSetDevice(dev);
+        else prev = -1;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
 spg_status_t hip_fail(spg_handle_t h, hipError_t e) {
     if (h) h->last_hip = (int)e;
     if (e == hipErrorOutOfMemory) return SPG_STATUS_ALLOC_FAILED;
@@ -390,7 +405,7 @@ spg_status_t wait_mirror(spg_handle_t h) {
 }
 
 spg_status_t read_scalars(spg_handle_t h, const int64_t* dev, int n, int64_t* out) {
-    if (n > PINNED_WORDS) return SPG_STATUS_INTERNAL_ERROR;
+    if (n > MIRROR_GEN_WORD) return SPG_STATUS_INTERNAL_ERROR;   // never reaches the generation word
     SPG_HIP(h, hipMemcpyAsync(h->pinned, dev, sizeof(int64_t) * n, hipMemcpyDeviceToHost, h->stream));
     SPG_HIP(h, stream_wait(h));
     for (int i = 0; i < n; ++i) out[i] = h->pinned[i];
@@ -994,8 +1009,13 @@ spg_status_t spg_create(spg_handle_t* handle, int hip_device) {
     if (!h) return SPG_STATUS_ALLOC_FAILED;
     h->device = dev;
     h->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-    hipError_t e = hipSetDevice(dev);
-    if (e == hipSuccess) e = hipHostMalloc((void**)&h->pinned, PINNED_WORDS * sizeof(int64_t), hipHostMallocDefault);
+    DeviceGuard dg_(dev);   // the handle's allocations on its device; the caller's device stays current
+    hipError_t e = dg_.err;
+    // fine-grained (coherent) host memory: the scan's system-scope stores of the scalars and
+    // then the generation word become visible to the polling host in that order
+    // (wait_mirror); the default host allocation is coarse-grained unless HIP_HOST_COHERENT=1
+    if (e == hipSuccess)
+        e = hipHostMalloc((void**)&h->pinned, PINNED_WORDS * sizeof(int64_t), hipHostMallocCoherent | hipHostMallocMapped);
     if (e == hipSuccess) std::memset(h->pinned, 0, PINNED_WORDS * sizeof(int64_t));
     if (e == hipSuccess) e = hipMalloc((void**)&h->spill_ctr, 256);
     if (e == hipSuccess) e = hipMemset(h->spill_ctr, 0, 256);
@@ -1044,7 +1064,8 @@ spg_status_t spg_plan(spg_handle_t h, const spg_csr_t* A, const spg_csr_t* B, sp
     if (alg == SPG_ALG3 && !(chunk_fraction > 0.0f && chunk_fraction <= 1.0f))
         return SPG_STATUS_INVALID_VALUE;
     if (workspace && !plan) return SPG_STATUS_INVALID_VALUE;
-    SPG_HIP(h, hipSetDevice(h->device));
+    DeviceGuard dg_(h->device);
+    SPG_HIP(h, dg_.err);
 
     spg_plan_s tmp;
     tmp.A = *A;
@@ -1094,7 +1115,7 @@ spg_status_t spg_plan(spg_handle_t h, const spg_csr_t* A, const spg_csr_t* B, sp
     if (tmp.use_tile) tmp.seg_len = 1;   // no cursor scratch on the tile path
     if (tmp.use_short && tmp.use_row && (tmp.alg == SPG_ALG2 || tmp.alg == SPG_ALG3)) {
         const int64_t nch = tmp.alg == SPG_ALG3 ? (int64_t)tmp.chunk_rows.size() - 1 : 1;
-        if (nch >= 1 && nch <= PINNED_WORDS - 16) tmp.nspc = nch;
+        if (nch >= 1 && nch <= MIRROR_GEN_WORD - 16) tmp.nspc = nch;   // words 16.. stay below the generation word
     }
     if (!workspace) {
         h->q_valid = true;
@@ -1139,7 +1160,8 @@ spg_status_t spg_num_products(spg_handle_t h, spg_plan_t p, int64_t* num_product
     if (!h) return SPG_STATUS_NOT_INITIALIZED;
     if (!p || !num_products) return SPG_STATUS_INVALID_VALUE;
     if (p->P < 0) {
-        SPG_HIP(h, hipSetDevice(h->device));
+        DeviceGuard dg_(h->device);
+        SPG_HIP(h, dg_.err);
         spg_status_t st;
         if ((st = products_total(h, p->A, p->B, &p->P))) return st;
     }
@@ -1152,7 +1174,8 @@ spg_status_t spg_symbolic(spg_handle_t h, spg_plan_t p, void* C_indptr, spg_inde
     if (!h) return SPG_STATUS_NOT_INITIALIZED;
     if (!p || !C_indptr || !nnzC) return SPG_STATUS_INVALID_VALUE;
     if (C_indptr_type != SPG_INDEX_32I && C_indptr_type != SPG_INDEX_64I) return SPG_STATUS_INVALID_VALUE;
-    SPG_HIP(h, hipSetDevice(h->device));
+    DeviceGuard dg_(h->device);
+    SPG_HIP(h, dg_.err);
     spg_status_t st;
     const bool i64 = p->A.indptr_type == SPG_INDEX_64I;
     if (fused_alg1(*p) && !p->fused_failed && p->use_row) {
@@ -1338,7 +1361,8 @@ spg_status_t spg_numeric(spg_handle_t h, spg_plan_t p, const void* alpha, spg_cs
     if (C->nnz != p->nnzC) return SPG_STATUS_INVALID_VALUE;
     if (p->nnzC > 0 && (!C->indices || !C->values)) return SPG_STATUS_INVALID_VALUE;
     if (p->nnzC == 0) return SPG_STATUS_SUCCESS;
-    SPG_HIP(h, hipSetDevice(h->device));
+    DeviceGuard dg_(h->device);
+    SPG_HIP(h, dg_.err);
     const bool i64 = p->A.indptr_type == SPG_INDEX_64I;
     const bool c64 = C->indptr_type == SPG_INDEX_64I;
     return dispatch_value(p->A.value_type, [&](auto tag) {
@@ -1360,7 +1384,8 @@ spg_status_t spg_spmv(spg_handle_t h, const spg_csr_t* A, const void* x, const v
     if (!alpha || !beta || (A->rows > 0 && !y) || (A->cols > 0 && A->nnz > 0 && !x))
         return SPG_STATUS_INVALID_VALUE;
     if (A->rows == 0) return SPG_STATUS_SUCCESS;
-    SPG_HIP(h, hipSetDevice(h->device));
+    DeviceGuard dg_(h->device);
+    SPG_HIP(h, dg_.err);
     const bool i64 = A->indptr_type == SPG_INDEX_64I;
     return dispatch_value(A->value_type, [&](auto tag) {
         using T = decltype(tag);
@@ -1403,7 +1428,8 @@ spg_status_t spg_validate_csr(spg_handle_t h, const spg_csr_t* M, int* is_canoni
     if (!is_canonical) return SPG_STATUS_INVALID_VALUE;
     spg_status_t st = check_csr(M);
     if (st) return st;
-    SPG_HIP(h, hipSetDevice(h->device));
+    DeviceGuard dg_(h->device);
+    SPG_HIP(h, dg_.err);
     if ((st = ensure_scratch(h, 256))) return st;
     int* flags = (int*)h->scratch;
     SPG_HIP(h, hipMemsetAsync(flags, 0, 2 * sizeof(int), h->stream));

@@ -115,6 +115,15 @@ def spgemm(a, b, alpha=1, alg=0, chunk_fraction=0.2, verbose=False):
     Returns:
         csr_matrix: C, with sorted column indices and structural entries kept.
     """
+    return _spgemm(a, b, alpha, alg, chunk_fraction, verbose)
+
+
+def _spgemm(a, b, alpha=1, alg=0, chunk_fraction=0.2, verbose=False, before_numeric=None):
+    """spgemm, plus `before_numeric`: a callable run after the symbolic pass and before the
+    numeric pass reads the values (the multi-GPU path waits there for B's values to arrive
+    over RCCL; spmm_amd.distributed).  With it the call takes the ctypes path (the native
+    shim runs both passes in one call); ALG1 runs it first (its count and numeric passes
+    are queued together)."""
     if not check_availability("spgemm"):
         raise RuntimeError("spgemm is not available.")
     assert a.ndim == b.ndim == 2
@@ -143,7 +152,10 @@ def spgemm(a, b, alpha=1, alg=0, chunk_fraction=0.2, verbose=False):
     dev = a.device
     h = _handle_for(a)
     cf = float(chunk_fraction)
-    fp = _fastpath.get()
+    fp = _fastpath.get() if before_numeric is None else None
+    if before_numeric is not None and algo == _lib.SPG_ALG1:
+        before_numeric()
+        before_numeric = None
     if fp is not None:   # the same sequence in one native call (csrc/fastpath.cpp)
         al = complex(alpha)
         st, data, indices, indptr, wsb, peak = fp.spgemm(
@@ -195,6 +207,8 @@ def spgemm(a, b, alpha=1, alg=0, chunk_fraction=0.2, verbose=False):
             data = torch.empty(nnzc, dtype=a.data.dtype, device=dev)
             vc = SpgCsr(m, n, nnzc, indptr.data_ptr(), indices.data_ptr() if nnzc else 0,
                         data.data_ptr() if nnzc else 0, _IT[indptr.dtype], _VT[data.dtype])
+            if before_numeric is not None:
+                before_numeric()
             check(lib.spg_numeric(h.ptr, plan, ctypes.byref(al), ctypes.byref(vc)), "spg_numeric")
         finally:
             lib.spg_plan_destroy(plan)

@@ -1,19 +1,24 @@
 """Multi-GPU C = A.B: 1-D row-block sharding of A, B broadcast over RCCL/xGMI.
 
 Rows of C depend only on the same rows of A and on all of B, so each rank
-owns a contiguous row block of A, receives B once, and writes its own C slab -- there is no
-cross-GPU reduction.  The only collectives are
+owns a contiguous row block of A, receives B, and writes its own C slab -- there is no
+cross-GPU reduction.  The collectives are
 
-* ``broadcast_csr``: B from ``src`` to every rank, as a 5-int64 metadata broadcast
-  followed by three payload broadcasts (indptr, indices, data) -- the protocol of the
-  reference's vendored sparse broadcast, modify_src/cupy-src/cupyx/distributed/
-  _nccl_comm.py:651-674 (metadata exchange :506-530), on torch.distributed (backend
-  "nccl" = RCCL on ROCm, "gloo" in CPU tests);
+* ``broadcast_csr``: B from ``src`` to every rank: one 6-int64 metadata broadcast (the
+  reference's sparse broadcast protocol, modify_src/cupy-src/cupyx/distributed/
+  _nccl_comm.py:651-674, metadata exchange :506-530), then the structure (row pointer and
+  column indices packed into ONE buffer) and the values (a second buffer), each a single
+  RCCL broadcast -- the reference groups its three payload broadcasts between
+  groupStart/groupEnd (:669); two packed buffers are the same "few large collectives" on
+  torch.distributed.  With ``async_values=True`` the values broadcast is left in flight and
+  its work handle returned, so the symbolic pass (which reads only B's structure) runs
+  while the values arrive (``spgemm_rowblock``'s ``before_numeric`` waits for them);
 * ``allgather_nnz``: every rank's nnz(C slab) -> global row-pointer offsets, when a
   stitched C is wanted.
 
-``row_blocks`` balances rows by the product-count prefix (equal FLOPs per rank); for
-uniform random inputs that is close to equal rows.
+``row_blocks`` balances rows by the product-count prefix (equal FLOPs per rank);
+``product_prefix`` computes that prefix on the device.  Backend "nccl" = RCCL on ROCm;
+"gloo" in the CPU tests.
 """
 from __future__ import annotations
 
@@ -23,33 +28,70 @@ import torch.distributed as dist
 
 from .sparse import csr_matrix
 
-_DT_CODE = {torch.float32: 0, torch.float64: 1}
+_DT_CODE = {torch.float32: 0, torch.float64: 1, torch.complex64: 2, torch.complex128: 3}
 _CODE_DT = {v: k for k, v in _DT_CODE.items()}
 _IP_CODE = {torch.int32: 0, torch.int64: 1}
 _CODE_IP = {v: k for k, v in _IP_CODE.items()}
 
 
-def broadcast_csr(M: csr_matrix | None, src: int, device, group=None) -> csr_matrix:
-    """Broadcast a CSR matrix held by rank `src` to every rank of `group`."""
+def _bytes_of(t: torch.Tensor) -> torch.Tensor:
+    return t.contiguous().view(-1).view(torch.uint8)
+
+
+def broadcast_csr(M: csr_matrix | None, src: int, device, group=None, async_values: bool = False):
+    """Broadcast a CSR matrix held by rank `src` to every rank of `group`.
+
+    Returns the matrix, or ``(matrix, work)`` with ``async_values=True``: the values
+    broadcast is still in flight and ``work.wait()`` orders the current stream after it
+    (``work`` is None when there is nothing to wait for)."""
     rank = dist.get_rank(group)
-    meta = torch.zeros(5, dtype=torch.int64, device=device)
+    meta = torch.zeros(6, dtype=torch.int64, device=device)
     if rank == src:
         meta = torch.tensor([M.shape[0], M.shape[1], M.nnz, _DT_CODE[M.data.dtype],
-                             _IP_CODE[M.indptr.dtype]], dtype=torch.int64, device=device)
+                             _IP_CODE[M.indptr.dtype], M.data.element_size()],
+                            dtype=torch.int64, device=device)
     dist.broadcast(meta, src, group=group)
-    rows, cols, nnz, dtc, ipc = (int(x) for x in meta.tolist())
+    rows, cols, nnz, dtc, ipc, _ = (int(x) for x in meta.tolist())
+    ipt = _CODE_IP[ipc]
+    ib = torch.empty(0, dtype=ipt).element_size()
+    sbytes = ib * (rows + 1) + 4 * nnz          # structure: indptr | indices
     if rank == src:
-        indptr, indices, data = (M.indptr.to(device), M.indices.to(device), M.data.to(device))
+        struct = torch.cat([_bytes_of(M.indptr.to(device)), _bytes_of(M.indices.to(device))])
+        data = M.data.to(device).contiguous()
     else:
-        indptr = torch.empty(rows + 1, dtype=_CODE_IP[ipc], device=device)
-        indices = torch.empty(nnz, dtype=torch.int32, device=device)
+        struct = torch.empty(sbytes, dtype=torch.uint8, device=device)
         data = torch.empty(nnz, dtype=_CODE_DT[dtc], device=device)
-    for t in (indptr, indices, data):
-        if t.numel():
-            dist.broadcast(t, src, group=group)
-    out = csr_matrix((data, indices, indptr), shape=(rows, cols), canonical=True)
-    out.indptr = indptr
-    return out
+    dist.broadcast(struct, src, group=group)
+    work = None
+    if nnz:
+        if async_values:
+            work = dist.broadcast(_bytes_of(data), src, group=group, async_op=True)
+        else:
+            dist.broadcast(_bytes_of(data), src, group=group)
+    indptr = struct[:ib * (rows + 1)].view(ipt)
+    indices = struct[ib * (rows + 1):].view(torch.int32)
+    out = csr_matrix._from_parts(data, indices, indptr, (rows, cols), canonical=True)
+    return (out, work) if async_values else out
+
+
+@torch.no_grad()
+def product_prefix(A: csr_matrix, b_indptr: torch.Tensor) -> torch.Tensor:
+    """int64 prefix of the per-row product counts of A.B (length rows + 1), on A's device:
+    P_i = sum over row i's entries k of B's row length (cusparse getNumProducts, per row)."""
+    blen = (b_indptr[1:] - b_indptr[:-1]).to(torch.int64)
+    prod = blen[A.indices.to(torch.int64)]
+    pref = torch.zeros(A.nnz + 1, dtype=torch.int64, device=prod.device)
+    torch.cumsum(prod, 0, out=pref[1:])
+    return pref[A.indptr.to(torch.int64)]   # entry prefix at each row start
+
+
+def row_slice(A: csr_matrix, r0: int, r1: int) -> csr_matrix:
+    """Rows [r0, r1) of A as its own CSR (copies: the slab owns its arrays)."""
+    ip = A.indptr
+    s, e = int(ip[r0]), int(ip[r1])
+    indptr = (ip[r0:r1 + 1] - ip[r0]).clone()
+    return csr_matrix._from_parts(A.data[s:e].clone(), A.indices[s:e].clone(), indptr,
+                                  (r1 - r0, A.shape[1]), canonical=True)
 
 
 def row_blocks(n_rows: int, world: int, product_prefix: np.ndarray | None = None):
@@ -78,10 +120,36 @@ def allgather_nnz(nnz: int, device, group=None) -> list[int]:
     return [int(t.item()) for t in out]
 
 
-def spgemm_rowblock(A_block: csr_matrix, B: csr_matrix, alg: int = 0, chunk_fraction: float = 0.2):
-    """This rank's C slab = A_block . B (row block r0:r1 of the global C)."""
+def spgemm_rowblock(A_block: csr_matrix, B: csr_matrix, alg: int = 0, chunk_fraction: float = 0.2,
+                    before_numeric=None):
+    """This rank's C slab = A_block . B (row block r0:r1 of the global C).  `before_numeric`
+    (e.g. the values broadcast's ``work.wait``) runs after the symbolic pass, before the
+    numeric pass reads B's values."""
     from . import cusparse
-    return cusparse.spgemm(A_block, B, alg=alg, chunk_fraction=chunk_fraction)
+    if before_numeric is None:
+        return cusparse.spgemm(A_block, B, alg=alg, chunk_fraction=chunk_fraction)
+    return cusparse._spgemm(A_block, B, alg=alg, chunk_fraction=chunk_fraction, before_numeric=before_numeric)
+
+
+def rowblock_setup(A: csr_matrix, b_indptr: torch.Tensor, world: int, rank: int):
+    """This rank's row block of A: the cut on the product-count prefix (equal products per
+    rank), the block as its own CSR, and its product count.  Returns ((r0, r1), A_block, P_r)."""
+    pref = product_prefix(A, b_indptr).cpu().numpy()
+    r0, r1 = row_blocks(A.shape[0], world, pref)[rank]
+    return (r0, r1), row_slice(A, r0, r1), int(pref[r1] - pref[r0])
+
+
+def rowblock_step(A_block: csr_matrix, B_src: csr_matrix | None, src: int, device, alg: int = 2,
+                  chunk_fraction: float = 0.2, multiply=None, group=None):
+    """One C = A.B step of the row-block scheme on this rank: B arrives from `src` (its
+    structure first; the values stay in flight through the symbolic pass), then this
+    rank's slab A_block . B.  `multiply(A_block, B, wait_values)` replaces the device
+    multiply (the gloo tests run the CPU oracle there).  Returns (C slab, B)."""
+    B, work = broadcast_csr(B_src, src, device, group, async_values=True)
+    wait = work.wait if work is not None else (lambda: None)
+    if multiply is not None:
+        return multiply(A_block, B, wait), B
+    return spgemm_rowblock(A_block, B, alg, chunk_fraction, before_numeric=wait), B
 
 
 def stitch_indptr(slab_indptrs, slab_nnz):

@@ -1,7 +1,9 @@
-"""The multi-GPU plumbing on CPU with the gloo backend (world_size 2): B broadcast
-(metadata + 3 payloads), row-block partition, nnz allgather and slab stitching.  The
-per-rank multiply is stood in for by the CPU oracle here (the device multiply is covered
-by the gpu tests); what is tested is the distributed bookkeeping."""
+"""The multi-GPU row-block path on CPU with the gloo backend (world_size 2), driven through
+the same functions bench.py's config-5 workload runs (spmm_amd.distributed.rowblock_setup
+and rowblock_step): B broadcast from rank 0 (metadata, packed structure, values left in
+flight), the product-prefix row cut, each rank's slab, the nnz allgather and the stitched
+row pointer.  The per-rank multiply is the CPU oracle (the device multiply is covered by the
+gpu tests); the stitched C must equal the oracle's C for the whole matrix, bit for bit."""
 import os
 import socket
 
@@ -19,7 +21,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, out):
+def _worker(rank, world, port, dtype, out):
     import scipy.sparse as sp
     import torch.distributed as dist
     from oracle import oracle
@@ -28,41 +30,59 @@ def _worker(rank, world, port, out):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    cpu = torch.device("cpu")
     n = 300
     rng = np.random.default_rng(7)
-    A = sp.random(n, n, density=0.03, format="csr", random_state=rng)
-    Bh = sp.random(n, n, density=0.03, format="csr", random_state=rng)
-    A.sort_indices(); Bh.sort_indices()
-    B0 = csr_matrix(Bh, device="cpu") if rank == 0 else None
-    B = distributed.broadcast_csr(B0, 0, torch.device("cpu"))
-    assert B.shape == Bh.shape and B.nnz == Bh.nnz
-    assert np.array_equal(B.indptr.numpy(), Bh.indptr)
-    assert np.array_equal(B.indices.numpy(), Bh.indices)
-    assert np.array_equal(B.data.numpy(), Bh.data)
-    pref = np.zeros(n + 1, np.int64)
-    pref[1:] = np.cumsum([sum(Bh.indptr[k + 1] - Bh.indptr[k] for k in A.indices[A.indptr[i]:A.indptr[i + 1]])
-                          for i in range(n)])
-    r0, r1 = distributed.row_blocks(n, world, pref)[rank]
-    p, j, x = oracle.spgemm(A[r0:r1], B.get(), keep_zeros=True, sort=True)
-    nnzs = distributed.allgather_nnz(len(j), torch.device("cpu"))
+    Ah = sp.random(n, n, density=0.03, format="csr", random_state=rng).astype(dtype)
+    Bh = sp.random(n, n, density=0.03, format="csr", random_state=rng).astype(dtype)
+    if np.issubdtype(dtype, np.complexfloating):
+        Ah.data = Ah.data + 1j * rng.standard_normal(Ah.nnz)
+        Bh.data = Bh.data + 1j * rng.standard_normal(Bh.nnz)
+    Ah.sort_indices(); Bh.sort_indices()
+    A = csr_matrix(Ah, device=cpu)
+    B_src = csr_matrix(Bh, device=cpu) if rank == 0 else None
+    # setup as bench.py: one broadcast for B's row lengths, the product-prefix cut
+    Bw = distributed.broadcast_csr(B_src, 0, cpu)
+    assert np.array_equal(Bw.indptr.numpy(), Bh.indptr) and np.array_equal(Bw.indices.numpy(), Bh.indices)
+    assert np.array_equal(Bw.data.numpy(), Bh.data)
+    (r0, r1), A_blk, P_r = distributed.rowblock_setup(A, Bw.indptr, world, rank)
+    assert P_r == oracle.num_products(Ah[r0:r1], Bh)
+
+    def multiply(A_b, B, wait_values):
+        wait_values()   # the values broadcast was left in flight
+        return oracle.spgemm(A_b.get(), B.get(), keep_zeros=True, sort=True)
+
+    (p, j, x), B = distributed.rowblock_step(A_blk, B_src, 0, cpu, multiply=multiply)
+    assert B.nnz == Bh.nnz
+    nnzs = distributed.allgather_nnz(len(j), cpu)
+    P_all = distributed.allgather_nnz(P_r, cpu)
     gathered = [None] * world
-    dist.all_gather_object(gathered, (p.tolist(), j.tolist(), x.tolist()))
+    dist.all_gather_object(gathered, (p.tolist(), j.tolist(), x.tolist(), (r0, r1)))
     if rank == 0:
         ip = distributed.stitch_indptr([g[0] for g in gathered], nnzs)
         jj = np.concatenate([np.asarray(g[1], np.int32) for g in gathered])
-        xx = np.concatenate([np.asarray(g[2]) for g in gathered])
-        rp, rj, rx = oracle.spgemm(A, Bh, keep_zeros=True, sort=True)
-        out["ok"] = bool(np.array_equal(ip, rp) and np.array_equal(jj, rj) and np.array_equal(xx, rx))
+        xx = np.concatenate([np.asarray(g[2], dtype=dtype) for g in gathered])
+        rp, rj, rx = oracle.spgemm(Ah, Bh, keep_zeros=True, sort=True)
+        blocks = [g[3] for g in gathered]
+        out["ok"] = bool(np.array_equal(ip, rp) and np.array_equal(jj, rj) and
+                         np.array_equal(xx.view(np.uint8), rx.view(np.uint8)))
+        out["blocks"] = blocks
+        out["products"] = P_all
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_rowblock_broadcast_gloo():
+@pytest.mark.parametrize("dtype", [np.float64, np.complex128])
+def test_rowblock_step_gloo(dtype):
     world = 2
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), dtype, out), nprocs=world, join=True)
     assert out.get("ok") is True
+    (a0, a1), (b0, b1) = out["blocks"]
+    assert a0 == 0 and a1 == b0 and b1 == 300   # contiguous cover of the rows
+    p0, p1 = out["products"]
+    assert abs(p0 - p1) <= 0.2 * (p0 + p1)     # cut on the product prefix: balanced
 
 
 def test_row_blocks_balanced():
@@ -72,3 +92,18 @@ def test_row_blocks_balanced():
     blocks = distributed.row_blocks(5, 2, pref)
     assert blocks[0][0] == 0 and blocks[-1][1] == 5
     assert all(b[0] <= b[1] for b in blocks)
+
+
+def test_product_prefix_matches_oracle():
+    import scipy.sparse as sp
+    from oracle import oracle
+    from spmm_amd import distributed
+    from spmm_amd.sparse import csr_matrix
+    rng = np.random.default_rng(3)
+    Ah = sp.random(200, 150, density=0.05, format="csr", random_state=rng)
+    Bh = sp.random(150, 120, density=0.05, format="csr", random_state=rng)
+    A = csr_matrix(Ah, device="cpu")
+    pref = distributed.product_prefix(A, torch.from_numpy(Bh.indptr.astype(np.int64))).numpy()
+    assert pref[0] == 0 and pref[-1] == oracle.num_products(Ah, Bh)
+    for i in (0, 17, 199):
+        assert pref[i + 1] - pref[i] == oracle.num_products(Ah[i:i + 1], Bh)

@@ -554,6 +554,7 @@ def test_side_stream_and_stream_switch():
     dA, dB = csr_matrix(A, device=_dev()), csr_matrix(B, device=_dev())
     ref = _oracle_ref(A, B)
     s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())   # dA, dB were copied in on the default stream
     with torch.cuda.stream(s):
         C1 = cusparse.spgemm(dA, dB, alg=1)
         got1 = (C1.indptr.cpu().numpy().astype(np.int64), C1.indices.cpu().numpy(), C1.data.cpu().numpy())
@@ -561,3 +562,45 @@ def test_side_stream_and_stream_switch():
     torch.cuda.synchronize()
     _assert_same(got1, ref)
     _assert_same((C2.indptr.cpu().numpy().astype(np.int64), C2.indices.cpu().numpy(), C2.data.cpu().numpy()), ref)
+
+
+def test_inputs_freed_while_side_stream_product_runs():
+    """An ALG1 call returns while its numeric pass is still queued on the side stream.
+    Inputs freed right after the call and their memory reused on another stream stay safe
+    when the caller records the side stream on them (torch's rule for any stream-ordered
+    library, cuSPARSE included): the caching allocator then holds the blocks until the
+    side stream's work is done."""
+    from spmm_amd import cusparse
+    from spmm_amd.sparse import csr_matrix
+    A = sp.random(8192, 8192, density=1e-3, format="csr", random_state=11)
+    B = sp.random(8192, 8192, density=1e-3, format="csr", random_state=12)
+    ref = _oracle_ref(A, B)
+    dA, dB = csr_matrix(A, device=_dev()), csr_matrix(B, device=_dev())
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        C = cusparse.spgemm(dA, dB, alg=1)
+    for t in (dA.data, dA.indices, dA.indptr, dB.data, dB.indices, dB.indptr):
+        t.record_stream(s)
+    del dA, dB
+    junk = [torch.full((1 << 20,), -1.0, dtype=torch.float64, device=_dev()) for _ in range(8)]
+    torch.cuda.synchronize()
+    del junk
+    _assert_same((C.indptr.cpu().numpy().astype(np.int64), C.indices.cpu().numpy(), C.data.cpu().numpy()), ref)
+
+
+@pytest.mark.skipif(not torch.cuda.is_available() or torch.cuda.device_count() < 2,
+                    reason="needs two GPUs")
+def test_product_on_non_current_device_keeps_current_device():
+    """The library switches to the handle's device for a call and restores the caller's
+    (cuSPARSE does not move the current device either)."""
+    from spmm_amd import cusparse
+    from spmm_amd.sparse import csr_matrix
+    A = sp.random(1024, 1024, density=1e-2, format="csr", random_state=1)
+    torch.cuda.set_device(0)
+    dA = csr_matrix(A, device="cuda:1")
+    C = cusparse.spgemm(dA, dA, alg=2)
+    assert torch.cuda.current_device() == 0
+    torch.cuda.synchronize(1)
+    _assert_same((C.indptr.cpu().numpy().astype(np.int64), C.indices.cpu().numpy(), C.data.cpu().numpy()),
+                 _oracle_ref(A, A))
