@@ -143,10 +143,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # one process per GPU; a rehearsal with more ranks than GPUs (SPG_DIST_BACKEND=gloo on a
+    # one-GPU box) puts several ranks on one device
+    local_dev = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("SPG_DIST_BACKEND", "nccl")   # nccl = RCCL on ROCm
+        dist.init_process_group(backend, **({"device_id": dev} if backend == "nccl" else {}))
 
     from spmm_amd import _lib, cusparse, distributed, gen
     from spmm_amd.sparse import csr_matrix
@@ -258,7 +262,7 @@ def main():
 
     # ---- per-phase device times (separate, instrumented pass after the timed region): HIP
     # events on the library's stream, which is torch's current stream
-    h = _lib.get_handle(local)
+    h = _lib.get_handle(local_dev)
     h.set_stream(torch.cuda.current_stream(dev).cuda_stream)
     h.set_timing(True)
     reps = 10 if cfg_name == "2" else 2

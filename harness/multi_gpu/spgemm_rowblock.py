@@ -5,14 +5,14 @@ N = 262144, density 1e-3, 8 x MI355X).
 Launch:  python -m torch.distributed.run --nproc-per-node G --master-addr 127.0.0.1 \\
              harness/multi_gpu/spgemm_rowblock.py --n 262144 --density 1e-3
 
-* strong scaling: the global N x N problem is fixed, rank r owns rows [r0, r1) (equal rows;
-  uniform inputs have equal expected products per row);
-* every rank draws its own row block of A with spmm_amd.gen.random_csr(row_offset=r0)
-  (row r of a block is row r0 + r of the full matrix); rank 0 draws B and broadcasts it
-  (5 x int64 metadata + 3 payload broadcasts, cupyx/distributed/_nccl_comm.py:651-674),
-  timed separately;
-* the timed step is each rank's own spgemm (no collective inside); GFLOPS = sum_r 2 P_r /
-  max_r t_r; allgather of the per-rank nnz gives the global row-pointer offsets;
+* strong scaling: the global N x N problem is fixed; every rank draws the whole A (the same
+  seed everywhere), rank 0 draws B; one broadcast of B gives every rank B's row lengths,
+  and rank r keeps the rows [r0, r1) cut on the product-count prefix (equal products per
+  rank, spmm_amd.distributed.rowblock_setup);
+* a timed step is spmm_amd.distributed.rowblock_step: B broadcast from rank 0 (metadata, one
+  packed structure buffer, the values left in flight through the symbolic pass) and this
+  rank's slab; GFLOPS = sum_r 2 P_r / max_r t_r; the broadcast alone is timed beside it;
+  allgather of the per-rank nnz gives the global row-pointer offsets;
 * --check S: S sampled rows per rank are recomputed on the host with the CPU oracle
   (tests/ oracle, parity check only) and compared bit for bit.
 Prints one JSON line on rank 0.
@@ -48,36 +48,49 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    local_dev = local % max(1, torch.cuda.device_count())   # (a gloo rehearsal may share a GPU)
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("SPG_DIST_BACKEND", "nccl")   # nccl = RCCL on ROCm
+        dist.init_process_group(backend, **({"device_id": dev} if backend == "nccl" else {}))
 
     n = args.n
-    r0, r1 = distributed.row_blocks(n, world)[rank]
-    A = gen.random_csr(r1 - r0, n, args.density, seed=args.seed, device=dev, row_offset=r0)
+    A = gen.random_csr(n, n, args.density, seed=args.seed, device=dev)
+    B0 = gen.random_csr(n, n, args.density, seed=args.seed + 1, device=dev) if rank == 0 or world == 1 else None
+    bcast_ms = 0.0
     if world > 1:
-        B0 = gen.random_csr(n, n, args.density, seed=args.seed + 1, device=dev) if rank == 0 else None
-        torch.cuda.synchronize(); dist.barrier()
-        t0 = time.perf_counter()
-        B = distributed.broadcast_csr(B0, 0, dev)
-        torch.cuda.synchronize(); dist.barrier()
-        bcast_ms = (time.perf_counter() - t0) * 1e3
-        del B0
+        Bw = distributed.broadcast_csr(B0, 0, dev)
+        (r0, r1), A, P = distributed.rowblock_setup(A, Bw.indptr, world, rank)
+        del Bw
+        ts = []
+        for _ in range(2):
+            torch.cuda.synchronize(); dist.barrier()
+            t0 = time.perf_counter()
+            Bt = distributed.broadcast_csr(B0, 0, dev)
+            torch.cuda.synchronize(); dist.barrier()
+            ts.append(time.perf_counter() - t0)
+            del Bt
+        bcast_ms = float(np.median(ts)) * 1e3
+
+        def step():
+            return distributed.rowblock_step(A, B0, 0, dev, args.alg, args.chunk_fraction)
     else:
-        B = gen.random_csr(n, n, args.density, seed=args.seed + 1, device=dev)
-        bcast_ms = 0.0
-    P = cusparse.num_products(A, B)
+        r0, r1 = 0, n
+        P = cusparse.num_products(A, B0)
+
+        def step():
+            return distributed.spgemm_rowblock(A, B0, args.alg, args.chunk_fraction), B0
     C = None
     for _ in range(args.warmup):
-        C = distributed.spgemm_rowblock(A, B, args.alg, args.chunk_fraction)
+        C, B = step()
         del C
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        C = distributed.spgemm_rowblock(A, B, args.alg, args.chunk_fraction)
+        C, B = step()
     torch.cuda.synchronize()
     t = time.perf_counter() - t0
     peak = cusparse.last_stats.peak_bytes

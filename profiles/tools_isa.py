@@ -1,3 +1,5 @@
+# Dev tool: per-kernel instruction mix of a device .s file (hipcc --cuda-device-only -S).
+# usage: python profiles/tools_isa.py <file.s> <kernel-name regex> [count]
 import re, sys
 from collections import Counter
 s = open(sys.argv[1]).read()

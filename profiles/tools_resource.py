@@ -1,5 +1,7 @@
+# Dev tool: VGPR / occupancy / LDS / scratch per kernel from -Rpass-analysis=kernel-resource-usage.
+# usage (from profiles/): python tools_resource.py [name filter]
 import re, subprocess, sys
-cmd = "hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Iinclude -Ispmm_amd/csrc -c spmm_amd/csrc/spgemm.hip -o /tmp/x.o -Rpass-analysis=kernel-resource-usage"
+cmd = "hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -I../include -I../spmm_amd/csrc -c ../spmm_amd/csrc/spgemm.hip -o /tmp/x.o -Rpass-analysis=kernel-resource-usage"
 out = subprocess.run(cmd, shell=True, capture_output=True, text=True).stderr
 cur = None
 rows = []

@@ -87,3 +87,18 @@ def test_rowblock_runner_single_gpu():
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["sampled_rows_bad"] == 0 and line["nnzC"] > 0
+
+
+def test_dpeak_sampler_sees_the_product():
+    """The harness's free-memory sampler (profiling.profile_op_gpu, the reference's
+    free0 - min(free), SpGEMM_alg_comparison/profiler.py:82-101) sees the product's
+    allocations: the dense_vs_sparseGEMM N=8192 density 1e-2 row reports about the
+    library's own peak (workspace + C, ~470 MB), not 0."""
+    from spmm_amd import gen, profiling
+    from spmm_amd.sparse import csr_matrix
+    Ah, Bh = gen.scipy_pair(8192, 1e-2, seed=42)
+    A, B = csr_matrix(Ah, device="cuda:0"), csr_matrix(Bh, device="cuda:0")
+    A @ B   # warm the handle and the allocator
+    r = profiling.profile_op_gpu("sparse", lambda: A @ B)
+    assert r.lib_peak_bytes and r.lib_peak_bytes > 4e8
+    assert r.peak_vram >= 0.8 * r.lib_peak_bytes, (r.peak_vram, r.lib_peak_bytes)
