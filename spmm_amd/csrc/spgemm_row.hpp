@@ -43,7 +43,8 @@ template <int R_, int LCAP_, int WPB_> struct RowCfg {
     static constexpr int LCAP = LCAP_;               // products in flagged words (<= WAVE)
     static constexpr int NW = 512;                   // bitmap words: <= 16384 columns
     static constexpr int WPB = WPB_;                 // waves per block
-    static constexpr int MKB = (PREG + 511) / 512 * 512;   // marker bytes
+    static constexpr int MKC = 16;                    // marker bytes per lane (>= R)
+    static constexpr int MKB = WAVE * MKC;            // marker bytes
     static_assert(LCAP <= WAVE, "one list entry per lane");
 };
 using RowSmall = RowCfg<10, 64, 4>;
@@ -61,12 +62,15 @@ template <typename T, typename IP> struct alignas(8) JRec<T, IP, false> {
 };
 
 template <typename T, typename IP, typename G, bool VALS, int SCAP = 0> struct RowLds {
-    uint32_t bits[G::NW];
-    uint16_t wpre[G::NW];          // exclusive popcount prefix | 0x8000 for flagged words
+    union {                        // the bitmap, expanded in place after pass 1 into
+        uint32_t bits[G::NW];      //   (word, exclusive popcount prefix | 0x8000 for a
+        uint2 bw[G::NW];           //   flagged word): one 8-byte read gives a position
+    };
     uint32_t dupw[G::NW / 32];     // one bit per bitmap word: a column of it was hit twice
     JRec<T, IP, VALS> jr[WAVE];    // per A entry: B row start, first product, value
     union {                        // phases of one row that never overlap:
-        int8_t mk[G::MKB];         //   lane -> A-entry markers of every chunk (pass 1)
+        uint8_t mk[G::MKB];        //   lane -> A-entry markers of every chunk (pass 1),
+                                   //   transposed: product t at 16 * (t % 64) + t / 64
         struct {                   //   flagged-word products in product order (fix-up)
             T lx[VALS ? G::LCAP : 1];
             int32_t lc[VALS ? G::LCAP : 1];
@@ -169,19 +173,21 @@ __device__ __forceinline__ void row_pass(Lds& S, int l, int cnt, int off, int P,
     bits4[2 * l] = make_uint4(0u, 0u, 0u, 0u);
     bits4[2 * l + 1] = make_uint4(0u, 0u, 0u, 0u);
     if (l < G::NW / 32) S.dupw[l] = 0u;
-#pragma unroll
-    for (int q = 0; q < (NC * WAVE + 511) / 512; ++q)
-        reinterpret_cast<uint64_t*>(S.mk)[q * WAVE + l] = 0ull;
+    static_assert(NC <= G::MKC, "one marker byte per chunk and lane");
+    reinterpret_cast<uint4*>(S.mk)[l] = make_uint4(0u, 0u, 0u, 0u);
     wsync();
-    if (cnt > 0) S.mk[off] = (int8_t)(l + 1);
+    if (cnt > 0) S.mk[((off & (WAVE - 1)) * G::MKC) | (off >> 6)] = (uint8_t)(l + 1);
     wsync();
     // lane -> A entry + 1 of each product (marker bytes + DPP max scans carried across
-    // chunks; the first product always has a marker, so every src >= 1)
+    // chunks; the first product always has a marker, so every src >= 1); a lane's markers
+    // of all chunks come with one 16-byte LDS read
     unsigned src[NC];
     {
+        const uint4 m4 = reinterpret_cast<const uint4*>(S.mk)[l];
+        const uint32_t mw[4] = {m4.x, m4.y, m4.z, m4.w};
         unsigned mrk[NC];
 #pragma unroll
-        for (int r = 0; r < NC; ++r) mrk[r] = (uint8_t)S.mk[r * WAVE + l];
+        for (int r = 0; r < NC; ++r) mrk[r] = (mw[r >> 2] >> (8 * (r & 3))) & 0xffu;
         unsigned carry = 0;
 #pragma unroll
         for (int r = 0; r < NC; ++r) {
@@ -239,7 +245,9 @@ __device__ __forceinline__ void row_pass(Lds& S, int l, int cnt, int off, int P,
     wsync();
     // (counting) distinct columns = products - repeated hits: no bitmap popcount
     if (!VALS) o.nnz = P - ndup;
-    // popcount prefix over this lane's 8 contiguous words, word flags in bit 15
+    // popcount prefix over this lane's 8 contiguous words, word flags in bit 15; the words
+    // and their prefixes go back as (word, prefix) pairs over the same LDS (every lane's
+    // reads are one instruction ahead of any lane's writes)
     if constexpr (VALS) {
         const uint4 q0 = bits4[2 * l], q1 = bits4[2 * l + 1];
         const int c0 = __popc(q0.x), c1 = __popc(q0.y), c2 = __popc(q0.z), c3 = __popc(q0.w);
@@ -251,12 +259,12 @@ __device__ __forceinline__ void row_pass(Lds& S, int l, int cnt, int off, int P,
         const int p0 = pincl - mine, p1 = p0 + c0, p2 = p1 + c1, p3 = p2 + c2, p4 = p3 + c3,
                   p5 = p4 + c4, p6 = p5 + c5, p7 = p6 + c6;
         auto f = [&](int p, int i) { return (uint32_t)p | (((fl >> i) & 1u) << 15); };
-        uint4 w;
-        w.x = f(p0, 0) | (f(p1, 1) << 16);
-        w.y = f(p2, 2) | (f(p3, 3) << 16);
-        w.z = f(p4, 4) | (f(p5, 5) << 16);
-        w.w = f(p6, 6) | (f(p7, 7) << 16);
-        reinterpret_cast<uint4*>(S.wpre)[l] = w;
+        wsync();
+        uint4* bw4 = reinterpret_cast<uint4*>(S.bw);
+        bw4[4 * l + 0] = make_uint4(q0.x, f(p0, 0), q0.y, f(p1, 1));
+        bw4[4 * l + 1] = make_uint4(q0.z, f(p2, 2), q0.w, f(p3, 3));
+        bw4[4 * l + 2] = make_uint4(q1.x, f(p4, 4), q1.y, f(p5, 5));
+        bw4[4 * l + 3] = make_uint4(q1.z, f(p6, 6), q1.w, f(p7, 7));
         wsync();
     }
     // products in flagged words: their number decides the spill; (VALS) their list
@@ -267,9 +275,9 @@ __device__ __forceinline__ void row_pass(Lds& S, int l, int cnt, int off, int P,
 #pragma unroll
         for (int r = 0; r < NC; ++r) {
             const int cc = col[r] < 0 ? 0 : col[r];
-            const uint32_t pw = S.wpre[cc >> 5];
-            const int p = (int)(pw & 0x7fffu) + __popc(S.bits[cc >> 5] & ((1u << (cc & 31)) - 1u));
-            o.cp[r] = col[r] < 0 ? -1 : (cc | (p << CP_POS) | (int)((pw >> 15) << 28));
+            const uint2 bw = S.bw[cc >> 5];
+            const int p = (int)(bw.y & 0x7fffu) + __popc(bw.x & ((1u << (cc & 31)) - 1u));
+            o.cp[r] = col[r] < 0 ? -1 : (cc | (p << CP_POS) | (int)(((bw.y >> 15) & 1u) << 28));
         }
         if (anydup) {
 #pragma unroll
