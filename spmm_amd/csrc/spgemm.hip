@@ -4,6 +4,7 @@
 // (ALG1 single pass, ALG2 two phase, ALG3 chunked two phase) and type dispatch to the
 // kernels in spgemm_kernels.hpp.  No HIP or C++ type crosses the ABI.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <atomic>
@@ -268,6 +269,23 @@ struct PhaseTimer {
         if (!b) { h->pool.push_back(a); return; }
         (void)hipEventRecord(b, h->stream);
         h->pending.push_back({phase, a, b});
+    }
+};
+
+// Device time of ONE kernel launch (the numeric phases, the roofline's kernel): the events
+// go into the launch's own dispatch packet (hipExtLaunchKernelGGL), so the interval is the
+// kernel's run time; hipEventRecord markers around a launch add gaps of their own (3-4 us
+// on the 28 us numeric pass of config 2).  Null events (timing off) record nothing.
+struct KernelTimer {
+    spg_handle_t h;
+    int phase;
+    hipEvent_t a = nullptr, b = nullptr;
+    KernelTimer(spg_handle_t h_, int phase_) : h(h_), phase(phase_) {
+        if (!h->timing || !(a = take_event(h))) return;
+        if (!(b = take_event(h))) { h->pool.push_back(a); a = nullptr; }
+    }
+    ~KernelTimer() {
+        if (a && b) h->pending.push_back({phase, a, b});
     }
 };
 
@@ -632,11 +650,12 @@ spg_status_t run_numeric_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_t
         return SPG_STATUS_INTERNAL_ERROR;   // the tile path runs through tile_numeric
     } else if (p.use_short && p.nspc > 0 && !UB) {
         {
-            PhaseTimer pt(h, SPG_PHASE_NUMERIC);
-            hipLaunchKernelGGL((k_row<T, IP, OFF, ROW_NUM, RowSmall>), dim3((unsigned)grid_for(n, RowSmall::WPB * ROW_PAIR)),
-                               dim3(RowSmall::WPB * WAVE), 0, h->stream, r0, n, p.B.cols, Ap, Aj, Ax, Bp, Bj, Bx,
-                               off, cj, cx, alpha, p.row_cnt, p.spill + r0, (int32_t*)(p.cspill + chunk),
-                               (int)ROW_LISTED, (int64_t)0, (const int64_t*)nullptr);
+            KernelTimer kt(h, SPG_PHASE_NUMERIC);
+            hipExtLaunchKernelGGL((k_row<T, IP, OFF, ROW_NUM, RowSmall>), dim3((unsigned)grid_for(n, RowSmall::WPB * ROW_PAIR)),
+                                  dim3(RowSmall::WPB * WAVE), 0, h->stream, kt.a, kt.b, 0, r0, n, p.B.cols, Ap, Aj, Ax,
+                                  Bp, Bj, Bx, off, cj, cx, alpha, p.row_cnt, p.spill + r0, (int32_t*)(p.cspill + chunk),
+                                  (int)ROW_LISTED, (int64_t)0, (const int64_t*)nullptr,
+                                  (unsigned long long*)nullptr, (int64_t)0);
             SPG_LAUNCHED(h);
         }
         // the general kernel only for a chunk whose count pass listed rows
@@ -786,17 +805,17 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
         if (nch > 1 && (st = tile_sym_chunk<IP>(h, p, c))) return st;
         const int64_t r0 = tile_chunk_r0(p, c), n = tile_chunk_r1(p, c) - r0;
         if (n <= 0) continue;
-        PhaseTimer pt(h, SPG_PHASE_NUMERIC);
+        KernelTimer kt(h, SPG_PHASE_NUMERIC);
         // dense accumulator when the tile fits one window; round groups (tile_variant())
         const bool dense = (1 << p.tws) <= TILE_CAP && tile_variant().dense;
         const int ru = tile_variant().ru;
         auto launch = [&](auto dn, auto rn) {
             constexpr bool DN = decltype(dn)::value;
             constexpr int RN = decltype(rn)::value;
-            hipLaunchKernelGGL((k_tile<T, IP, DN, RN>), dim3(tile_grid(n * p.G)), dim3(TILE_WPB * WAVE), 0, h->stream,
-                               r0, n, p.tws, p.G, Ap, Aj, Ax, p.B.rows, (const uint32_t*)p.brec,
-                               (const int32_t*)p.tptr, (const uint32_t*)p.bitmap, (const int64_t*)p.item_cnt,
-                               cj, cx, alpha, tile_variant().diag);
+            hipExtLaunchKernelGGL((k_tile<T, IP, DN, RN>), dim3(tile_grid(n * p.G)), dim3(TILE_WPB * WAVE), 0,
+                                  h->stream, kt.a, kt.b, 0, r0, n, p.tws, p.G, Ap, Aj, Ax, p.B.rows,
+                                  (const uint32_t*)p.brec, (const int32_t*)p.tptr, (const uint32_t*)p.bitmap,
+                                  (const int64_t*)p.item_cnt, cj, cx, alpha, tile_variant().diag);
         };
         constexpr int UF = sizeof(T) > 8 ? 4 : 8;
         using D1 = std::integral_constant<bool, true>;
@@ -848,13 +867,14 @@ spg_status_t alg1_fused_run(spg_handle_t h, spg_plan_s& p, void* cp) {
                                                p.scalars, false);
             if (st) return st;
         }
-        PhaseTimer pn(h, SPG_PHASE_NUMERIC);
-        hipLaunchKernelGGL((k_row<T, IP, OUT, ROW_NUM, RowSmall>), dim3(grid), dim3(RowSmall::WPB * WAVE), 0,
-                           h->stream, (int64_t)0, p.A.rows, p.B.cols, (const IP*)p.A.indptr,
-                           (const int32_t*)p.A.indices, (const T*)p.A.values, (const IP*)p.B.indptr,
-                           (const int32_t*)p.B.indices, (const T*)p.B.values, (const OUT*)cp, p.tj, (T*)p.tx,
-                           (T)1, p.row_cnt, p.spill, spill_counts(p, true), (int)ROW_LISTED,
-                           std::max<int64_t>(p.cap, 1), (const int64_t*)p.scalars);
+        KernelTimer kt(h, SPG_PHASE_NUMERIC);
+        hipExtLaunchKernelGGL((k_row<T, IP, OUT, ROW_NUM, RowSmall>), dim3(grid), dim3(RowSmall::WPB * WAVE), 0,
+                              h->stream, kt.a, kt.b, 0, (int64_t)0, p.A.rows, p.B.cols, (const IP*)p.A.indptr,
+                              (const int32_t*)p.A.indices, (const T*)p.A.values, (const IP*)p.B.indptr,
+                              (const int32_t*)p.B.indices, (const T*)p.B.values, (const OUT*)cp, p.tj, (T*)p.tx,
+                              (T)1, p.row_cnt, p.spill, spill_counts(p, true), (int)ROW_LISTED,
+                              std::max<int64_t>(p.cap, 1), (const int64_t*)p.scalars, (unsigned long long*)nullptr,
+                              (int64_t)0);
         SPG_LAUNCHED(h);
         return SPG_STATUS_SUCCESS;
     }
