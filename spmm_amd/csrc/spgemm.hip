@@ -200,7 +200,7 @@ inline bool want_tile(const spg_csr_t& A, const spg_csr_t& B, int& tws, int& G) 
 
 // grid of a tile kernel over `tasks` wave tasks: a multiple of 8 (XCD-aware block ids)
 inline unsigned tile_grid(int64_t tasks) {
-    const int64_t nb = std::max<int64_t>(1, std::min<int64_t>(grid_for(tasks, TILE_WPB), 1 << 22));
+    const int64_t nb = std::max<int64_t>(1, std::min<int64_t>(grid_for(tasks, TILE_WPB), 1 << 26));
     return (unsigned)((nb + 7) / 8 * 8);
 }
 

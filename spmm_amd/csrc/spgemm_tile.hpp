@@ -613,8 +613,8 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile(
             T* __restrict__ xrow = Cx + obase + wb;
             for (int p = l; p < wn; p += WAVE) {
                 const uint32_t c = S.tag[p];
-                crow[p] = (int32_t)c;
                 const T val = S.acc[p];
+                crow[p] = (int32_t)c;
                 xrow[p] = (alpha == (T)1) ? val : mul_rn(alpha, val);
             }
             wsync();
