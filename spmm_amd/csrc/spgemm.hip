@@ -289,6 +289,15 @@ struct KernelTimer {
     }
 };
 
+// A launch timed by KernelTimer (every kernel of the timed phases: the phase time is the
+// sum of its kernels' device times; marker events around launches drift once ext-launch
+// events are on the stream).
+template <typename K, typename... Args>
+inline void timed_launch(spg_handle_t h, int phase, K kernel, dim3 grid, dim3 block, Args... args) {
+    KernelTimer kt(h, phase);
+    hipExtLaunchKernelGGL(kernel, grid, block, 0, h->stream, kt.a, kt.b, 0, args...);
+}
+
 spg_status_t check_csr(const spg_csr_t* M) {
     if (!M) return SPG_STATUS_INVALID_VALUE;
     if (M->rows < 0 || M->cols < 0 || M->nnz < 0) return SPG_STATUS_INVALID_VALUE;
@@ -328,9 +337,8 @@ spg_status_t launch_scan(spg_handle_t h, int64_t n, const IN* in, OUT* out,
     const int64_t tiles = scan_tiles(n);
     if (zero_status)
         SPG_HIP(h, hipMemsetAsync(status, 0, sizeof(unsigned long long) * (size_t)(tiles + 1), h->stream));
-    PhaseTimer pt(h, SPG_PHASE_SCAN);
-    hipLaunchKernelGGL((k_scan_lb<OUT, IN>), dim3((unsigned)tiles), dim3(BLOCK), 0, h->stream, n, in, out,
-                       status, scal, move_cnt, move_dst, host_mirror, mirror_gen, mirror_n, seed);
+    timed_launch(h, SPG_PHASE_SCAN, k_scan_lb<OUT, IN>, dim3((unsigned)tiles), dim3(BLOCK), n, in, out, status, scal,
+                 move_cnt, move_dst, host_mirror, mirror_gen, mirror_n, seed);
     SPG_LAUNCHED(h);
     return SPG_STATUS_SUCCESS;
 }
@@ -591,13 +599,12 @@ spg_status_t run_symbolic_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_
         return SPG_STATUS_INTERNAL_ERROR;   // the tile path runs through tile_symbolic
     } else if (p.use_short && p.nspc > 0) {
         // k_row counts every row (spills by the chunked loop) and lists this chunk's spills
-        PhaseTimer pt(h, SPG_PHASE_SYMBOLIC);
-        hipLaunchKernelGGL((k_row<double, IP, int64_t, ROW_SYM, RowSmall>),
-                           dim3((unsigned)grid_for(n, RowSmall::WPB * ROW_PAIR)), dim3(RowSmall::WPB * WAVE), 0,
-                           h->stream, r0, n, p.B.cols, Ap, Aj, (const double*)nullptr, Bp, Bj,
+        timed_launch(h, SPG_PHASE_SYMBOLIC, k_row<double, IP, int64_t, ROW_SYM, RowSmall>,
+                           dim3((unsigned)grid_for(n, RowSmall::WPB * ROW_PAIR)), dim3(RowSmall::WPB * WAVE),
+                           r0, n, p.B.cols, Ap, Aj, (const double*)nullptr, Bp, Bj,
                            (const double*)nullptr, (const int64_t*)nullptr, (int32_t*)nullptr, (double*)nullptr,
                            1.0, p.row_cnt, p.spill + r0, (int32_t*)(p.cspill + chunk), (int)ROW_COUNT_ALL,
-                           (int64_t)0, (const int64_t*)nullptr);
+                           (int64_t)0, (const int64_t*)nullptr, (unsigned long long*)nullptr, (int64_t)0);
     } else if (p.use_short) {
         int32_t* cnt = spill_counts(p, false);
         int32_t* l1 = p.spill;
@@ -718,13 +725,13 @@ spg_status_t tile_build_index(spg_handle_t h, spg_plan_s& p) {
     const int32_t* Bj = (const int32_t*)p.B.indices;
     const int R = 1 << (p.twss - p.tws);
     {
-        PhaseTimer ps(h, SPG_PHASE_SPILL);
-        hipLaunchKernelGGL(k_tile_index<IP>, dim3((unsigned)grid_for(p.B.rows, 4)), dim3(256), 0, h->stream,
-                           p.B.rows, Bp, Bj, p.tws, p.G, p.tidx);
+        timed_launch(h, SPG_PHASE_SPILL, k_tile_index<IP>, dim3((unsigned)grid_for(p.B.rows, 4)), dim3(256), p.B.rows,
+                     Bp, Bj, p.tws, p.G, p.tidx);
         SPG_LAUNCHED(h);
         const int64_t n2 = p.B.rows * p.G + p.G;
-        hipLaunchKernelGGL(k_bt_count, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(grid_for(n2, 256), 65536))),
-                           dim3(256), 0, h->stream, p.B.rows, p.G, R, (const uint2*)p.tidx, p.tptr, p.sidx);
+        timed_launch(h, SPG_PHASE_SPILL, k_bt_count,
+                     dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(grid_for(n2, 256), 65536))), dim3(256),
+                     p.B.rows, p.G, R, (const uint2*)p.tidx, p.tptr, p.sidx);
         SPG_LAUNCHED(h);
     }
     spg_status_t st = launch_scan<int32_t, int32_t>(h, bt_entries(p), p.tptr, p.tptr, bt_scan_status(p),
@@ -742,8 +749,7 @@ template <typename IP>
 spg_status_t tile_sym_chunk(spg_handle_t h, spg_plan_s& p, int64_t c) {
     const int64_t r0 = tile_chunk_r0(p, c), n = tile_chunk_r1(p, c) - r0;
     if (n > 0) {
-        PhaseTimer pt(h, SPG_PHASE_SYMBOLIC);
-        hipLaunchKernelGGL(k_tile_sym<IP>, dim3(tile_grid(n * sym_tiles(p))), dim3(TILE_WPB * WAVE), 0, h->stream,
+        timed_launch(h, SPG_PHASE_SYMBOLIC, k_tile_sym<IP>, dim3(tile_grid(n * sym_tiles(p))), dim3(TILE_WPB * WAVE),
                            r0, n, p.tws, p.G, p.twss, (const IP*)p.A.indptr, (const int32_t*)p.A.indices,
                            (const IP*)p.B.indptr, (const int32_t*)p.B.indices, (const uint32_t*)p.sidx, p.bitmap,
                            p.item_cnt);
@@ -759,9 +765,8 @@ spg_status_t tile_sym_chunk(spg_handle_t h, spg_plan_s& p, int64_t c) {
 template <typename OUT>
 spg_status_t tile_rowptr_chunk(spg_handle_t h, spg_plan_s& p, int64_t c, void* cp) {
     const int64_t r0 = tile_chunk_r0(p, c), n = tile_chunk_r1(p, c) - r0;
-    PhaseTimer pt(h, SPG_PHASE_SCAN);
-    hipLaunchKernelGGL(k_items_to_rowptr<OUT>, dim3((unsigned)grid_for(n + 1, 256)), dim3(256), 0, h->stream, n,
-                       p.G, (const int64_t*)p.item_cnt, (OUT*)cp + r0);
+    timed_launch(h, SPG_PHASE_SCAN, k_items_to_rowptr<OUT>, dim3((unsigned)grid_for(n + 1, 256)), dim3(256), n, p.G,
+                 (const int64_t*)p.item_cnt, (OUT*)cp + r0);
     SPG_LAUNCHED(h);
     return SPG_STATUS_SUCCESS;
 }
@@ -793,9 +798,8 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
     const T* Ax = (const T*)p.A.values;
     const T* Bx = (const T*)p.B.values;
     if (!p.brec_built) {
-        PhaseTimer ps(h, SPG_PHASE_SPILL);
-        hipLaunchKernelGGL((k_bt_pack<T, IP>), dim3((unsigned)grid_for(p.B.rows, 4)), dim3(256), 0, h->stream,
-                           p.B.rows, Bp, Bj, Bx, p.tws, (const int32_t*)p.tptr, (uint32_t*)p.brec);
+        timed_launch(h, SPG_PHASE_SPILL, k_bt_pack<T, IP>, dim3((unsigned)grid_for(p.B.rows, 4)), dim3(256), p.B.rows,
+                     Bp, Bj, Bx, p.tws, (const int32_t*)p.tptr, (uint32_t*)p.brec);
         SPG_LAUNCHED(h);
         p.brec_built = true;
     }
@@ -848,9 +852,8 @@ spg_status_t alg1_fused_run(spg_handle_t h, spg_plan_s& p, void* cp) {
         if (!p.counts_ready) {
             if (h->spill_ctr_dirty) SPG_HIP(h, hipMemsetAsync(h->spill_ctr, 0, sizeof(int32_t), h->stream));
             h->spill_ctr_dirty = true;
-            PhaseTimer ps(h, SPG_PHASE_SYMBOLIC);
-            hipLaunchKernelGGL((k_row<double, IP, OUT, ROW_SYM, RowSmall>), dim3(grid), dim3(RowSmall::WPB * WAVE), 0,
-                               h->stream, (int64_t)0, p.A.rows, p.B.cols, (const IP*)p.A.indptr,
+            timed_launch(h, SPG_PHASE_SYMBOLIC, k_row<double, IP, OUT, ROW_SYM, RowSmall>, dim3(grid), dim3(RowSmall::WPB * WAVE),
+                               (int64_t)0, p.A.rows, p.B.cols, (const IP*)p.A.indptr,
                                (const int32_t*)p.A.indices, (const double*)nullptr, (const IP*)p.B.indptr,
                                (const int32_t*)p.B.indices, (const double*)nullptr, (const OUT*)nullptr,
                                (int32_t*)nullptr, (double*)nullptr, 1.0, p.row_cnt, p.spill, h->spill_ctr,

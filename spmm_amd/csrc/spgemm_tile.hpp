@@ -482,8 +482,9 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile(
                     const int nchg = min(TILE_MK, Pb - gb);
                     const uint4 mrow = reinterpret_cast<const uint4*>(S.mk)[l];
                     for (int c0 = 0; c0 < nchg; c0 += U * WAVE) {
-                        // U chunks at once, or U/2 when no more hold products (a wave-uniform
-                        // choice: no empty slots scanned and loaded for short batches)
+                        // U, 3U/4 or U/2 chunks at once, the fewest that hold the group's
+                        // remaining products (a wave-uniform choice: short batches scan and
+                        // load few empty slots)
                         const int nu = min(U, (nchg - c0 + WAVE - 1) >> 6);
                         auto step = [&](auto nuc) {
                             constexpr int NU = decltype(nuc)::value;
@@ -564,7 +565,8 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile(
                                 }
                             }
                         };
-                        if (nu > U / 2) step(std::integral_constant<int, U>{});
+                        if (nu > 3 * U / 4) step(std::integral_constant<int, U>{});
+                        else if (nu > U / 2) step(std::integral_constant<int, 3 * U / 4>{});
                         else step(std::integral_constant<int, U / 2>{});
                         if (seq < 4096u) {   // re-arm the tag space (very long items only)
                             wsync();
