@@ -82,6 +82,7 @@ struct spg_plan_s {
     int twss = 10;                  // log2 of the symbolic tile width (>= tws, <= 16)
     bool counts_ready = false;      // a symbolic pass has completed (counts / offsets valid)
     unsigned long long* lb = nullptr;   // ALG1 single pass: per-row look-back status words
+    void* ext = nullptr;            // ALG1 on k_row: every A entry's B row extent (RowExt)
     bool alg1_fused = false;        // C's arrays were written compact into tj/tx by one pass
     bool fused_failed = false;      // the single pass met a row it cannot take
     bool scaled_in_place = false;   // spg_numeric scaled the workspace result by alpha
@@ -161,6 +162,8 @@ inline const TileVariant& tile_variant() {
 inline int64_t grid_for(int64_t rows, int per_block) { return (rows + per_block - 1) / per_block; }
 
 inline int64_t scan_tiles(int64_t n) { return n > 0 ? (n + SCAN_TILE - 1) / SCAN_TILE : 1; }
+// 64-row groups (ALG1 on k_row: one published prefix per group)
+inline int64_t row_groups(int64_t n) { return (n + WAVE - 1) / WAVE; }
 
 // Rows of the expected shape go to the short-row kernel first; the rest (and every row it
 // rejects) to the general windowed kernels.  Only a scheduling choice: results are the
@@ -440,7 +443,7 @@ spg_status_t read_scalars(spg_handle_t h, const int64_t* dev, int n, int64_t* ou
 
 struct Layout {
     size_t scalars = 0, row_cnt = 0, seg = 0, spill = 0, status = 0, ub = 0, tj = 0, tx = 0;
-    size_t tptr = 0, sidx = 0, items = 0, bitmap = 0, brec = 0, total = 0;
+    size_t tptr = 0, sidx = 0, items = 0, bitmap = 0, brec = 0, ext = 0, total = 0;
 };
 
 // Tile path row chunks: ALG3's chunks (items and bitmaps are sized by the largest one and
@@ -470,7 +473,7 @@ inline bool fused_alg1(const spg_plan_s& p) {
 inline size_t status_words(const spg_plan_s& p) {
     return 2 * (size_t)(scan_tiles(p.A.rows) + 1) +
            (p.use_tile ? (size_t)scan_tiles(tile_items(p)) + 1 + (size_t)scan_tiles(bt_entries(p)) + 1 : 0) +
-           (fused_alg1(p) ? (size_t)grid_for(p.A.rows, ShortSmall::WPB) + 1 : 0);
+           (fused_alg1(p) ? (size_t)std::max<int64_t>(grid_for(p.A.rows, ShortSmall::WPB), row_groups(p.A.rows)) + 1 : 0);
 }
 inline unsigned long long* item_scan_status(const spg_plan_s& p) {
     return p.scan_status + 2 * (scan_tiles(p.A.rows) + 1);
@@ -502,6 +505,10 @@ Layout make_layout(const spg_plan_s& p) {
         // single pass: C itself, `cap` entries (an estimate); upper-bound path: P entries
         const int64_t n = fused_alg1(p) ? p.cap : p.P;
         if (!fused_alg1(p)) { L.ub = off; off = align_up(off + sizeof(int64_t) * (size_t)(p.A.rows + 1)); }
+        if (fused_alg1(p) && p.use_row) {
+            const size_t eb = p.A.indptr_type == SPG_INDEX_64I ? sizeof(RowExt<int64_t>) : sizeof(RowExt<int32_t>);
+            L.ext = off; off = align_up(off + eb * (size_t)std::max<int64_t>(p.A.nnz, 1));
+        }
         L.tj = off; off = align_up(off + sizeof(int32_t) * (size_t)std::max<int64_t>(n, 1));
         L.tx = off; off = align_up(off + vbytes(p.A.value_type) * (size_t)std::max<int64_t>(n, 1));
     }
@@ -527,6 +534,7 @@ void carve(spg_plan_s& p, const Layout& L) {
     }
     if (p.alg == SPG_ALG1 && !p.use_tile) {
         if (!fused_alg1(p)) p.ub = (int64_t*)(p.ws + L.ub);
+        if (fused_alg1(p) && p.use_row) p.ext = (void*)(p.ws + L.ext);
         p.tj = (int32_t*)(p.ws + L.tj);
         p.tx = (void*)(p.ws + L.tx);
     }
@@ -604,7 +612,8 @@ spg_status_t run_symbolic_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_
                            r0, n, p.B.cols, Ap, Aj, (const double*)nullptr, Bp, Bj,
                            (const double*)nullptr, (const int64_t*)nullptr, (int32_t*)nullptr, (double*)nullptr,
                            1.0, p.row_cnt, p.spill + r0, (int32_t*)(p.cspill + chunk), (int)ROW_COUNT_ALL,
-                           (int64_t)0, (const int64_t*)nullptr, (unsigned long long*)nullptr, (int64_t)0);
+                           (int64_t)0, (const int64_t*)nullptr, (unsigned long long*)nullptr, (int64_t)0,
+                           (RowExt<IP>*)nullptr, RowScan<int64_t>{});
     } else if (p.use_short) {
         int32_t* cnt = spill_counts(p, false);
         int32_t* l1 = p.spill;
@@ -616,7 +625,8 @@ spg_status_t run_symbolic_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_
                                    h->stream, r0, n, p.B.cols, Ap, Aj, (const double*)nullptr, Bp, Bj,
                                    (const double*)nullptr, (const int64_t*)nullptr, (int32_t*)nullptr,
                                    (double*)nullptr, 1.0, p.row_cnt, l1, cnt, 0, (int64_t)0,
-                                   (const int64_t*)nullptr);
+                                   (const int64_t*)nullptr, (unsigned long long*)nullptr, (int64_t)0,
+                                   (RowExt<IP>*)nullptr, RowScan<int64_t>{});
             else
                 hipLaunchKernelGGL((k_short<double, IP, int64_t, SHORT_SYM, ShortSmall>),
                                    dim3((unsigned)grid_for(n, ShortSmall::WPB)), dim3(ShortSmall::WPB * WAVE), 0,
@@ -662,7 +672,7 @@ spg_status_t run_numeric_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_t
                                   dim3(RowSmall::WPB * WAVE), 0, h->stream, kt.a, kt.b, 0, r0, n, p.B.cols, Ap, Aj, Ax,
                                   Bp, Bj, Bx, off, cj, cx, alpha, p.row_cnt, p.spill + r0, (int32_t*)(p.cspill + chunk),
                                   (int)ROW_LISTED, (int64_t)0, (const int64_t*)nullptr,
-                                  (unsigned long long*)nullptr, (int64_t)0);
+                                  (unsigned long long*)nullptr, (int64_t)0, (RowExt<IP>*)nullptr, RowScan<OFF>{});
             SPG_LAUNCHED(h);
         }
         // the general kernel only for a chunk whose count pass listed rows
@@ -681,7 +691,8 @@ spg_status_t run_numeric_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_t
                 hipLaunchKernelGGL((k_row<T, IP, OFF, ROW_NUM, RowSmall>), dim3((unsigned)grid_for(n, RowSmall::WPB * ROW_PAIR)),
                                    dim3(RowSmall::WPB * WAVE), 0, h->stream, r0, n, p.B.cols, Ap, Aj, Ax, Bp, Bj,
                                    Bx, off, cj, cx, alpha, p.row_cnt, l1, cnt, 0, (int64_t)0,
-                                   (const int64_t*)nullptr);
+                                   (const int64_t*)nullptr, (unsigned long long*)nullptr, (int64_t)0,
+                                   (RowExt<IP>*)nullptr, RowScan<OFF>{});
             else
                 hipLaunchKernelGGL((k_short<T, IP, OFF, MODE, ShortSmall>), dim3((unsigned)grid_for(n, ShortSmall::WPB)),
                                    dim3(ShortSmall::WPB * WAVE), 0, h->stream, r0, n, p.B.cols, Ap, Aj, Ax, Bp, Bj,
@@ -847,37 +858,42 @@ spg_status_t alg1_fused_run(spg_handle_t h, spg_plan_s& p, void* cp) {
         // spills are counted in the handle's counter, which the scan moves into
         // scalars[5] and re-arms
         const unsigned grid = (unsigned)grid_for(p.A.rows, RowSmall::WPB * ROW_PAIR);
+        // the numeric launch's scan words: ticket + tile status, then the group prefixes
         unsigned long long* status = p.scan_status + scan_tiles(p.A.rows) + 1;
-        const int64_t nstatus = scan_tiles(p.A.rows) + 1;
+        const int64_t nscan = scan_tiles(p.A.rows);
+        const int64_t nstatus = nscan + 1 + row_groups(p.A.rows);
+        RowExt<IP>* ext = (RowExt<IP>*)p.ext;
+        RowScan<OUT> sa{nscan, (OUT*)cp, status, status + nscan + 1, p.scalars, nullptr, nullptr, nullptr, 0, 0};
         if (!p.counts_ready) {
             if (h->spill_ctr_dirty) SPG_HIP(h, hipMemsetAsync(h->spill_ctr, 0, sizeof(int32_t), h->stream));
             h->spill_ctr_dirty = true;
-            timed_launch(h, SPG_PHASE_SYMBOLIC, k_row<double, IP, OUT, ROW_SYM, RowSmall>, dim3(grid), dim3(RowSmall::WPB * WAVE),
+            timed_launch(h, SPG_PHASE_SYMBOLIC, k_row<double, IP, int64_t, ROW_SYM, RowSmall>, dim3(grid), dim3(RowSmall::WPB * WAVE),
                                (int64_t)0, p.A.rows, p.B.cols, (const IP*)p.A.indptr,
                                (const int32_t*)p.A.indices, (const double*)nullptr, (const IP*)p.B.indptr,
-                               (const int32_t*)p.B.indices, (const double*)nullptr, (const OUT*)nullptr,
+                               (const int32_t*)p.B.indices, (const double*)nullptr, (const int64_t*)nullptr,
                                (int32_t*)nullptr, (double*)nullptr, 1.0, p.row_cnt, p.spill, h->spill_ctr,
-                               (int)ROW_COUNT_ALL, (int64_t)0, (const int64_t*)nullptr, status, nstatus);
+                               (int)ROW_COUNT_ALL, (int64_t)0, (const int64_t*)nullptr, status, nstatus,
+                               ext, RowScan<int64_t>{});
             SPG_LAUNCHED(h);
-            spg_status_t st = launch_scan<OUT>(h, p.A.rows, (const int64_t*)p.row_cnt, (OUT*)cp, status,
-                                               p.scalars, false, h->spill_ctr, p.scalars + 5, h->pinned,
-                                               ++h->mirror_gen, 2);   // words 0, 1 (+ 5: the move)
-            if (st) return st;
+            // the scan blocks hand the spill count over (to scalars[5]), re-arm the counter and
+            // mirror total / overflow / spills into the pinned buffer
+            sa.move_cnt = h->spill_ctr;
+            sa.move_dst = p.scalars + 5;
+            sa.host_mirror = h->pinned;
+            sa.mirror_gen = ++h->mirror_gen;
+            sa.mirror_n = 2;   // words 0, 1 (+ 5: the move)
             h->spill_ctr_dirty = false;
-        } else {   // repeated call: the first scan already moved the spill count
+        } else {   // repeated call: the first call already moved the spill count
             SPG_HIP(h, hipMemsetAsync(status, 0, sizeof(unsigned long long) * (size_t)nstatus, h->stream));
-            spg_status_t st = launch_scan<OUT>(h, p.A.rows, (const int64_t*)p.row_cnt, (OUT*)cp, status,
-                                               p.scalars, false);
-            if (st) return st;
         }
         KernelTimer kt(h, SPG_PHASE_NUMERIC);
-        hipExtLaunchKernelGGL((k_row<T, IP, OUT, ROW_NUM, RowSmall>), dim3(grid), dim3(RowSmall::WPB * WAVE), 0,
-                              h->stream, kt.a, kt.b, 0, (int64_t)0, p.A.rows, p.B.cols, (const IP*)p.A.indptr,
-                              (const int32_t*)p.A.indices, (const T*)p.A.values, (const IP*)p.B.indptr,
-                              (const int32_t*)p.B.indices, (const T*)p.B.values, (const OUT*)cp, p.tj, (T*)p.tx,
-                              (T)1, p.row_cnt, p.spill, spill_counts(p, true), (int)ROW_LISTED,
-                              std::max<int64_t>(p.cap, 1), (const int64_t*)p.scalars, (unsigned long long*)nullptr,
-                              (int64_t)0);
+        hipExtLaunchKernelGGL((k_row<T, IP, OUT, ROW_LB, RowSmall>), dim3((unsigned)(nscan + grid)),
+                              dim3(RowSmall::WPB * WAVE), 0, h->stream, kt.a, kt.b, 0, (int64_t)0, p.A.rows, p.B.cols,
+                              (const IP*)p.A.indptr, (const int32_t*)p.A.indices, (const T*)p.A.values,
+                              (const IP*)p.B.indptr, (const int32_t*)p.B.indices, (const T*)p.B.values,
+                              (const OUT*)nullptr, p.tj, (T*)p.tx, (T)1, p.row_cnt, p.spill, spill_counts(p, true),
+                              (int)ROW_LISTED, std::max<int64_t>(p.cap, 1), (const int64_t*)nullptr,
+                              (unsigned long long*)nullptr, (int64_t)0, ext, sa);
         SPG_LAUNCHED(h);
         return SPG_STATUS_SUCCESS;
     }

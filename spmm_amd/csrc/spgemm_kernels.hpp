@@ -747,23 +747,31 @@ constexpr int SCAN_TILE = BLOCK * SCAN_ITEMS;   // 2048
 // every word read_scalars fills)
 constexpr int MIRROR_GEN_WORD = 16 + 1024;
 
-template <typename OUT, typename IN = int64_t>
-__global__ __launch_bounds__(BLOCK) void k_scan_lb(int64_t n, const IN* in, OUT* out,
-                                                   unsigned long long* __restrict__ status,
-                                                   int64_t* __restrict__ scalars,
-                                                   int32_t* __restrict__ move_cnt = nullptr,
-                                                   int64_t* __restrict__ move_dst = nullptr,
-                                                   int64_t* __restrict__ host_mirror = nullptr,
-                                                   int64_t mirror_gen = 0, int mirror_n = 0,
-                                                   const int64_t* seed = nullptr) {
-    constexpr unsigned long long VMASK = (1ull << 62) - 1;
-    __shared__ long long wsum[WPB];
-    __shared__ long long prefix_s;
-    __shared__ int bid_s;
+constexpr unsigned long long SCAN_VMASK = (1ull << 62) - 1;
+constexpr unsigned long long GPRE_READY = 1ull << 63;
+
+// LDS of one scan tile (a block of BLOCK threads)
+struct ScanLds {
+    long long wsum[WPB];
+    long long prefix;
+};
+
+// One tile of the scan, tile index `bid` (tiles below it have started).  `st` = the tile
+// status words (status + 1).  With `gpre`, the exclusive prefix at every 64-element group
+// start also goes to gpre[group] | GPRE_READY (agent-scope stores: k_row's ALG1 numeric
+// pass reads its rows' offsets from them while the scan runs beside it).
+template <typename OUT, typename IN>
+__device__ __forceinline__ void scan_tile(int64_t bid, int64_t n, const IN* in, OUT* out,
+                                          unsigned long long* __restrict__ st, int64_t* __restrict__ scalars,
+                                          int32_t* __restrict__ move_cnt, int64_t* __restrict__ move_dst,
+                                          int64_t* __restrict__ host_mirror, int64_t mirror_gen, int mirror_n,
+                                          const int64_t* seed, ScanLds& L,
+                                          unsigned long long* __restrict__ gpre = nullptr) {
+    static_assert(SCAN_ITEMS * 8 == WAVE, "8 threads per 64-element group");
+    constexpr unsigned long long VMASK = SCAN_VMASK;
+    long long* wsum = L.wsum;
+    long long& prefix_s = L.prefix;
     const int tid = threadIdx.x, l = lane_id(), wv = tid >> 6;
-    if (tid == 0) bid_s = (int)atomicAdd(&status[0], 1ull);
-    __syncthreads();
-    const int64_t bid = bid_s;
     const int64_t base = bid * SCAN_TILE + (int64_t)tid * SCAN_ITEMS;
     long long v[SCAN_ITEMS];
     long long tsum = 0;
@@ -781,7 +789,6 @@ __global__ __launch_bounds__(BLOCK) void k_scan_lb(int64_t n, const IN* in, OUT*
         if (q < wv) wbase += wsum[q];
         btot += wsum[q];
     }
-    unsigned long long* st = status + 1;
     if (wv == 0) {
         long long prefix = 0;
         if (bid == 0) {
@@ -817,6 +824,9 @@ __global__ __launch_bounds__(BLOCK) void k_scan_lb(int64_t n, const IN* in, OUT*
     }
     __syncthreads();
     long long run = prefix_s + wbase + incl - tsum;
+    if (gpre && (tid & 7) == 0 && base < n)
+        __hip_atomic_store(&gpre[base >> 6], GPRE_READY | (unsigned long long)run, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
     for (int j = 0; j < SCAN_ITEMS; ++j) {
         if (base + j < n) out[base + j] = (OUT)run;
@@ -857,6 +867,23 @@ __global__ __launch_bounds__(BLOCK) void k_scan_lb(int64_t n, const IN* in, OUT*
         if (mirror_n > 0)
             __hip_atomic_store(&host_mirror[MIRROR_GEN_WORD], mirror_gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+}
+
+template <typename OUT, typename IN = int64_t>
+__global__ __launch_bounds__(BLOCK) void k_scan_lb(int64_t n, const IN* in, OUT* out,
+                                                   unsigned long long* __restrict__ status,
+                                                   int64_t* __restrict__ scalars,
+                                                   int32_t* __restrict__ move_cnt = nullptr,
+                                                   int64_t* __restrict__ move_dst = nullptr,
+                                                   int64_t* __restrict__ host_mirror = nullptr,
+                                                   int64_t mirror_gen = 0, int mirror_n = 0,
+                                                   const int64_t* seed = nullptr) {
+    __shared__ ScanLds L;
+    __shared__ int bid_s;
+    if (threadIdx.x == 0) bid_s = (int)atomicAdd(&status[0], 1ull);
+    __syncthreads();
+    scan_tile<OUT, IN>(bid_s, n, in, out, status + 1, scalars, move_cnt, move_dst, host_mirror, mirror_gen,
+                       mirror_n, seed, L);
 }
 
 // ---------------------------------------------------------------------------------------

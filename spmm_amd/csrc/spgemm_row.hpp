@@ -23,12 +23,14 @@
 // predicate in every mode, so the symbolic and numeric passes spill the same rows -- to the
 // general kernel (k_symbolic / k_numeric over the spill list).
 //
-// MODES: ROW_SYM counts (ALG2/3 symbolic), ROW_NUM writes at C's row pointer (ALG2/3
-// numeric), ROW_LB is the ALG1 single pass: every row publishes its count into a 64-ary
-// arrival tree (LbTree), reads the exclusive prefix of its row from at most 4 tree levels
-// (one load per lane per level, all issued before pass 2), and writes C's row pointer,
-// columns and values in one launch.  Spilled rows still publish their count (the count-only
-// loop below) and get their values from a k_numeric launch over the spill list afterwards.
+// MODES: ROW_SYM counts (ALG2/3 symbolic, and ALG1's count pass, which also leaves every
+// A entry's B row extent behind for the numeric pass), ROW_NUM writes at C's row pointer
+// (ALG2/3 numeric), ROW_LB is ALG1's numeric pass with the row-pointer scan inside it: its
+// first blocks scan the count pass's row counts (C's row pointer, one published prefix per
+// 64-row group, the host mirror), the rest take the rows, each at its group's prefix plus
+// the counts before it in the group (RowScan).  Spilled rows are counted by the count pass
+// (the count-only loop below) and get their values from a k_numeric launch over the spill
+// list afterwards.
 #pragma once
 
 #include "spgemm_kernels.hpp"
@@ -64,8 +66,8 @@ template <typename T, typename IP> struct alignas(8) JRec<T, IP, false> {
 template <typename T, typename IP, typename G, bool VALS, int SCAP = 0> struct RowLds {
     union {                        // the bitmap, expanded in place after pass 1 into
         uint32_t bits[G::NW];      //   (word, exclusive popcount prefix | 0x8000 for a
-        uint2 bw[G::NW];           //   flagged word): one 8-byte read gives a position
-    };
+        uint2 bw[VALS ? G::NW : 1];   // flagged word): one 8-byte read gives a position
+    };                             //   (numeric only: counting needs the bitmap alone)
     uint32_t dupw[G::NW / 32];     // one bit per bitmap word: a column of it was hit twice
     JRec<T, IP, VALS> jr[WAVE];    // per A entry: B row start, first product, value
     union {                        // phases of one row that never overlap:
@@ -78,9 +80,10 @@ template <typename T, typename IP, typename G, bool VALS, int SCAP = 0> struct R
         };
         int8_t marker[WAVE + 4];   //   count-only loop (one chunk at a time)
     };
-    // ALG1 pipeline: the previous row's output in position order, until its base is known
-    T sx[SCAP > 0 ? SCAP : 1];
-    uint16_t sc[SCAP > 0 ? SCAP : 1];
+    // ALG1 numeric with the scan inside: the row's group word and in-group count prefix,
+    // parked here (not in registers) until the row's output is ready
+    unsigned long long lb_gw;
+    long long lb_gsum;
 };
 
 // Value of any of the four types from lane j (j wave-uniform).
@@ -151,6 +154,59 @@ __device__ __forceinline__ RowFront<T, IP> row_front_load(int l, int64_t a0, int
     }
     return f;
 }
+// ALG1: the count pass leaves every A entry's B row extent behind (RowExt, parallel to A's
+// entries), so the numeric pass reads it in one load instead of A's column and then B's
+// row pointer (one dependent global load less per row).
+template <typename IP> struct alignas(sizeof(IP) == 8 ? 16 : 8) RowExt {
+    IP b0;
+    int32_t cnt;
+};
+template <bool VALS, typename T, typename IP>
+__device__ __forceinline__ RowFront<T, IP> row_front_ext(int l, int64_t a0, int nA, const RowExt<IP>* __restrict__ ext,
+                                                         const T* __restrict__ Ax) {
+    RowFront<T, IP> f{(IP)0, 0, (T)0};
+    if (l < nA) {
+        const RowExt<IP> e = ext[a0 + l];
+        f.b0 = e.b0;
+        f.cnt = e.cnt;
+        if (VALS) f.av = Ax[a0 + l];
+    }
+    return f;
+}
+
+// ALG1 numeric pass with the row-pointer scan inside it: blocks 0..nscan-1 scan the count
+// pass's row counts (scan_tile: C's row pointer, the total, the host mirror) and publish the
+// exclusive prefix of every 64-row group in gpre; the other blocks take the rows, each
+// row's offset = its group's prefix + the counts of the rows before it in the group.  A row
+// wave reads its group word when it starts and waits for it only when its output is ready
+// to leave (by then the scan is long done: it reads 8 bytes per row).  The scan blocks come
+// first in dispatch order and wait on nothing the row blocks produce.
+template <typename OFF> struct RowScan {
+    int64_t nscan;                     // scan tiles; 0: offsets come from Coff
+    OFF* out;                          // C's row pointer
+    unsigned long long* status;        // ticket word + tile status words, zero on entry
+    unsigned long long* gpre;          // group prefixes, zero on entry
+    int64_t* scalars;
+    int32_t* move_cnt;
+    int64_t* move_dst;
+    int64_t* host_mirror;
+    int64_t mirror_gen;
+    int mirror_n;
+};
+
+// the exclusive prefix of a row group: its published word (the scan blocks were dispatched
+// before every row block and wait on nothing the row blocks produce, so it arrives); the
+// wait stays in scalar registers (the row's output occupies the vector registers)
+__device__ __forceinline__ long long row_group_prefix(const unsigned long long* gp, unsigned long long gw) {
+    while (!(gw & GPRE_READY)) {
+        __builtin_amdgcn_s_sleep(2);
+        const unsigned long long v = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        gw = ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
+             (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    }
+    return (long long)(gw & SCAN_VMASK);
+}
+
 // ... then the flattened product offset of each entry goes to LDS.  Returns the row's
 // product count P (wave-uniform).
 template <bool VALS, typename T, typename IP, typename Lds>
@@ -165,7 +221,7 @@ __device__ __forceinline__ int row_front_commit(Lds& S, int l, const RowFront<T,
 // The register path for a row of P (1 <= P <= NC*64) products: bitmap, positions, the
 // flagged-word list and its fix-up.  o.take = false when the list overflows LCAP (the row
 // then goes to the general kernel; o.nnz is still its count).
-template <int NC, bool VALS, typename T, typename IP, typename G, typename Lds, int NCMAX>
+template <int NC, bool VALS, bool AVL, typename T, typename IP, typename G, typename Lds, int NCMAX>
 __device__ __forceinline__ void row_pass(Lds& S, int l, int cnt, int off, int P, const int32_t* __restrict__ Bj,
                                          const T* __restrict__ Bx, RowOut<T, NCMAX>& o) {
     static_assert(NC <= NCMAX, "chunks");
@@ -209,18 +265,23 @@ __device__ __forceinline__ void row_pass(Lds& S, int l, int cnt, int off, int P,
             j = jr1[src[r]];
         }
         idx[r] = t < P ? j.jb0 + (IP)(t - j.joff) : (IP)0;
-        if constexpr (VALS) av[r] = j.ja;
+        if constexpr (VALS && !AVL) av[r] = j.ja;
     }
     // every product of the row in flight at once
     int col[NC];
 #pragma unroll
     for (int r = 0; r < NC; ++r) col[r] = ld_idx(Bj, idx[r]);
-    if (VALS) {
+    if constexpr (VALS) {
         T bx[NC];
 #pragma unroll
         for (int r = 0; r < NC; ++r) bx[r] = ld_idx(Bx, idx[r]);
+        // (AVL) A's values from LDS while the gathers are in flight, not held in registers
+        // across them
 #pragma unroll
-        for (int r = 0; r < NC; ++r) o.prd[r] = mul_rn(av[r], bx[r]);
+        for (int r = 0; r < NC; ++r) {
+            if constexpr (AVL) o.prd[r] = mul_rn(jr1[src[r]].ja, bx[r]);
+            else o.prd[r] = mul_rn(av[r], bx[r]);
+        }
     }
 #pragma unroll
     for (int r = 0; r < NC; ++r)
@@ -335,14 +396,14 @@ __device__ __forceinline__ void row_pass(Lds& S, int l, int cnt, int off, int P,
 // P in [1, PREG]: the register path with the smallest chunk count that holds P, then
 // `then(o)` on its result -- inside each case, so the result of one case
 // never meets another's at a join (it would otherwise occupy registers for all five).
-template <bool VALS, typename T, typename IP, typename G, typename Lds, typename F>
+template <bool VALS, bool AVL, typename T, typename IP, typename G, typename Lds, typename F>
 __device__ __forceinline__ void row_dispatch(Lds& S, int l, int cnt, int off, int P, const int32_t* __restrict__ Bj,
                                              const T* __restrict__ Bx, F&& then) {
     static_assert(G::R == 10, "dispatch covers 10 chunks");
     auto run = [&](auto nct) {
         constexpr int NC = decltype(nct)::value;
         RowOut<T, NC> o;
-        row_pass<NC, VALS, T, IP, G>(S, l, cnt, off, P, Bj, Bx, o);
+        row_pass<NC, VALS, AVL, T, IP, G>(S, l, cnt, off, P, Bj, Bx, o);
         then(o);
     };
     switch ((P + WAVE - 1) / WAVE) {   // exact chunk counts where rows are common
@@ -367,7 +428,7 @@ __device__ __forceinline__ void row_dispatch(Lds& S, int l, int cnt, int off, in
 template <bool UNIT, typename T, int NCMAX, typename Lds>
 __device__ __forceinline__ void row_write_staged(Lds& S, int l, const RowOut<T, NCMAX>& o,
                                                  int32_t* __restrict__ crow, T* __restrict__ xrow, T alpha) {
-    constexpr int W = (int)(__builtin_offsetof(Lds, sx) / (sizeof(T) + 4));
+    constexpr int W = (int)(__builtin_offsetof(Lds, lb_gw) / (sizeof(T) + 4));
     T* sv = reinterpret_cast<T*>(&S);
     int32_t* sc = reinterpret_cast<int32_t*>(sv + W);
     wsync();   // row_pass's reads of these words are done
@@ -459,6 +520,11 @@ enum { ROW_COUNT_ALL = 1, ROW_LISTED = 2 };
 #define SPG_ROW_PAIR 1
 #endif
 constexpr int ROW_PAIR = SPG_ROW_PAIR;   // rows per wave (k_row)
+// A's values re-read from LDS after the gathers instead of held in registers across them
+// (ROW_LB only): fewer live registers, but measured 1.5 us slower on config 2's numeric pass
+#ifndef SPG_ROW_AVLDS
+#define SPG_ROW_AVLDS 0
+#endif
 // register budget: 5 waves per SIMD (<= 96 VGPRs) for 4- and 8-byte values
 template <typename T, typename IP, typename OFF, int MODE, typename G>
 __global__ __launch_bounds__(G::WPB * WAVE, sizeof(T) <= 8 ? 5 : 3) void k_row(
@@ -467,14 +533,25 @@ __global__ __launch_bounds__(G::WPB * WAVE, sizeof(T) <= 8 ? 5 : 3) void k_row(
     const int32_t* __restrict__ Bj, const T* __restrict__ Bx, const OFF* __restrict__ Coff,
     int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha, int64_t* __restrict__ row_cnt,
     int32_t* __restrict__ spill, int32_t* __restrict__ spill_count, int flags, int64_t cap,
-    const int64_t* __restrict__ scan_scal, unsigned long long* __restrict__ zero_words = nullptr,
-    int64_t nzero = 0) {
-    static_assert(MODE == ROW_SYM || MODE == ROW_NUM, "modes");
+    const int64_t* __restrict__ scan_scal, unsigned long long* __restrict__ zero_words, int64_t nzero,
+    RowExt<IP>* __restrict__ ext, RowScan<OFF> sa) {
+    static_assert(MODE == ROW_SYM || MODE == ROW_NUM || MODE == ROW_LB, "modes");
+    static_assert(G::WPB * WAVE == BLOCK, "scan tiles are blocks of BLOCK threads");
     constexpr bool VALS = MODE != ROW_SYM;
+    constexpr bool lb = MODE == ROW_LB;
+    constexpr bool AVL = lb && SPG_ROW_AVLDS;
     __shared__ __attribute__((aligned(16))) RowLds<T, IP, G, VALS> lds[G::WPB];
-    // (ALG1 count pass) block 0 zeroes the next launch's scan status words: no memset
-    if (zero_words && blockIdx.x == 0)
-        for (int64_t i = threadIdx.x; i < nzero; i += G::WPB * WAVE) zero_words[i] = 0ull;
+    // (ALG1 count pass) the next launch's scan status words are zeroed here: no memset
+    if (zero_words)
+        for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < nzero; i += (int64_t)gridDim.x * BLOCK)
+            zero_words[i] = 0ull;
+    if (lb && (int64_t)blockIdx.x < sa.nscan) {
+        __shared__ ScanLds scan_l;
+        scan_tile<OFF, int64_t>(blockIdx.x, nrows, row_cnt + row0, sa.out, sa.status + 1, sa.scalars,
+                                sa.move_cnt, sa.move_dst, sa.host_mirror, sa.mirror_gen, sa.mirror_n,
+                                nullptr, scan_l, sa.gpre);
+        return;
+    }
     const int l = lane_id();
     const int wv = uniform((int)(threadIdx.x >> 6));
     RowLds<T, IP, G, VALS>& S = lds[wv];
@@ -482,7 +559,7 @@ __global__ __launch_bounds__(G::WPB * WAVE, sizeof(T) <= 8 ? 5 : 3) void k_row(
     // ROW_PAIR consecutive rows per wave: both rows' fronts (A entries, B row extents) are
     // loaded before the first row is worked on, so the second row's dependent loads are
     // in flight during the first row's gathers and LDS work
-    const int64_t it0 = ((int64_t)blockIdx.x * G::WPB + wv) * ROW_PAIR;
+    const int64_t it0 = (((int64_t)blockIdx.x - (lb ? sa.nscan : 0)) * G::WPB + wv) * ROW_PAIR;
     if (it0 >= nrows) return;
     const int nr = (int)min((int64_t)ROW_PAIR, nrows - it0);
     int64_t a0s[ROW_PAIR + 1];
@@ -493,12 +570,42 @@ __global__ __launch_bounds__(G::WPB * WAVE, sizeof(T) <= 8 ? 5 : 3) void k_row(
     for (int q = 0; q < ROW_PAIR; ++q) {
         const int nAq = q < nr ? (int)(a0s[q + 1] - a0s[q]) : 0;
         const bool f = nAq > 0 && nAq <= WAVE && ncols > 0;
-        fr[q] = row_front_load<VALS, T, IP>(l, a0s[q], f ? nAq : 0, Aj, Ax, Bp);
+        if (lb) {
+            fr[q] = row_front_ext<VALS, T, IP>(l, a0s[q], f ? nAq : 0, ext, Ax);
+        } else {
+            fr[q] = row_front_load<VALS, T, IP>(l, a0s[q], f ? nAq : 0, Aj, Ax, Bp);
+            if (MODE == ROW_SYM && ext && f && l < nAq) ext[a0s[q] + l] = RowExt<IP>{fr[q].b0, fr[q].cnt};
+        }
+    }
+    // (lb) each row's group word and the counts of the rows before it in its group
+    unsigned long long gw[ROW_PAIR] = {};
+    int gc[ROW_PAIR] = {};   // (a row's count < 2^31: the low word of its int64 count)
+    if (lb) {
+#pragma unroll
+        for (int q = 0; q < ROW_PAIR; ++q) {
+            gw[q] = 0;
+            gc[q] = 0;
+            if (q < nr) {
+                const int64_t it = it0 + q, g0 = it & ~(int64_t)(WAVE - 1);
+                gw[q] = __hip_atomic_load(&sa.gpre[it >> 6], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                gc[q] = g0 + l < it ? reinterpret_cast<const int*>(row_cnt + row0 + g0 + l)[0] : 0;
+            }
+        }
     }
 
-    auto do_row = [&](int64_t row, int64_t a0, int nA, const RowFront<T, IP>& f) {
+    auto do_row = [&](int64_t row, int64_t a0, int nA, const RowFront<T, IP>& f, unsigned long long gwq,
+                      int gcq) {
         int64_t base = 0;
         bool room = true;
+        // (lb) wave-uniform from here on (scalar registers): the group word and the counts
+        // of the rows before this one in its group
+        if (lb) {
+            const int gsum = wave_incl_sum_dpp(gcq);
+            if (l == WAVE - 1) {
+                S.lb_gw = gwq;
+                S.lb_gsum = gsum;
+            }
+        }
         if (MODE == ROW_NUM) {
             base = (int64_t)Coff[row];
             if (cap > 0) room = (int64_t)Coff[row + 1] <= cap;
@@ -515,10 +622,20 @@ __global__ __launch_bounds__(G::WPB * WAVE, sizeof(T) <= 8 ? 5 : 3) void k_row(
         bool take = false;
         int nnz = 0;
         if (fits && P > 0) {
-            row_dispatch<VALS, T, IP, G>(S, l, f.cnt, off, P, Bj, Bx, [&](const auto& o) {
+            row_dispatch<VALS, AVL, T, IP, G>(S, l, f.cnt, off, P, Bj, Bx, [&](const auto& o) {
                 take = o.take;
                 nnz = o.nnz;
-                if (take && MODE == ROW_NUM && room) row_write(S, l, o, Cj + base, Cx + base, alpha);
+                if (take && lb) {
+                    const int64_t it = row - row0;
+                    const unsigned long long g = S.lb_gw;   // (all lanes read the same word)
+                    base = row_group_prefix(&sa.gpre[it >> 6],
+                                            ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(g >> 32)) << 32) |
+                                                (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)g)) +
+                           __builtin_amdgcn_readfirstlane((int)S.lb_gsum);
+                    const int64_t end = base + nnz;
+                    room = (cap <= 0 || end <= cap) && (sizeof(OFF) == 8 || end <= 2147483647LL);
+                }
+                if (take && VALS && room) row_write(S, l, o, Cj + base, Cx + base, alpha);
             });
         }
         if (!empty && !take) {
@@ -530,7 +647,8 @@ __global__ __launch_bounds__(G::WPB * WAVE, sizeof(T) <= 8 ? 5 : 3) void k_row(
     };
 #pragma unroll
     for (int q = 0; q < ROW_PAIR; ++q)
-        if (q < nr) do_row(row0 + it0 + q, a0s[q], (int)(a0s[q + 1] - a0s[q]), fr[q]);
+        if (q < nr) do_row(row0 + it0 + q, a0s[q], (int)(a0s[q + 1] - a0s[q]), fr[q], lb ? gw[q] : 0ull,
+                           lb ? gc[q] : 0);
 }
 
 }  // namespace spg
