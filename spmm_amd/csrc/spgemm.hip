@@ -608,7 +608,7 @@ spg_status_t run_symbolic_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_
     } else if (p.use_short && p.nspc > 0) {
         // k_row counts every row (spills by the chunked loop) and lists this chunk's spills
         timed_launch(h, SPG_PHASE_SYMBOLIC, k_row<double, IP, int64_t, ROW_SYM, RowSmall>,
-                           dim3((unsigned)grid_for(n, RowSmall::WPB * ROW_PAIR)), dim3(RowSmall::WPB * WAVE),
+                           dim3((unsigned)grid_for(n, RowSmall::WPB * row_pair<ROW_SYM>())), dim3(RowSmall::WPB * WAVE),
                            r0, n, p.B.cols, Ap, Aj, (const double*)nullptr, Bp, Bj,
                            (const double*)nullptr, (const int64_t*)nullptr, (int32_t*)nullptr, (double*)nullptr,
                            1.0, p.row_cnt, p.spill + r0, (int32_t*)(p.cspill + chunk), (int)ROW_COUNT_ALL,
@@ -621,7 +621,7 @@ spg_status_t run_symbolic_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_
             PhaseTimer pt(h, SPG_PHASE_SYMBOLIC);
             if (p.use_row)
                 hipLaunchKernelGGL((k_row<double, IP, int64_t, ROW_SYM, RowSmall>),
-                                   dim3((unsigned)grid_for(n, RowSmall::WPB * ROW_PAIR)), dim3(RowSmall::WPB * WAVE), 0,
+                                   dim3((unsigned)grid_for(n, RowSmall::WPB * row_pair<ROW_SYM>())), dim3(RowSmall::WPB * WAVE), 0,
                                    h->stream, r0, n, p.B.cols, Ap, Aj, (const double*)nullptr, Bp, Bj,
                                    (const double*)nullptr, (const int64_t*)nullptr, (int32_t*)nullptr,
                                    (double*)nullptr, 1.0, p.row_cnt, l1, cnt, 0, (int64_t)0,
@@ -668,7 +668,7 @@ spg_status_t run_numeric_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_t
     } else if (p.use_short && p.nspc > 0 && !UB) {
         {
             KernelTimer kt(h, SPG_PHASE_NUMERIC);
-            hipExtLaunchKernelGGL((k_row<T, IP, OFF, ROW_NUM, RowSmall>), dim3((unsigned)grid_for(n, RowSmall::WPB * ROW_PAIR)),
+            hipExtLaunchKernelGGL((k_row<T, IP, OFF, ROW_NUM, RowSmall>), dim3((unsigned)grid_for(n, RowSmall::WPB * row_pair<ROW_NUM>())),
                                   dim3(RowSmall::WPB * WAVE), 0, h->stream, kt.a, kt.b, 0, r0, n, p.B.cols, Ap, Aj, Ax,
                                   Bp, Bj, Bx, off, cj, cx, alpha, p.row_cnt, p.spill + r0, (int32_t*)(p.cspill + chunk),
                                   (int)ROW_LISTED, (int64_t)0, (const int64_t*)nullptr,
@@ -688,7 +688,7 @@ spg_status_t run_numeric_rows(spg_handle_t h, spg_plan_s& p, int64_t r0, int64_t
         {
             PhaseTimer pt(h, SPG_PHASE_NUMERIC);
             if (p.use_row && !UB)
-                hipLaunchKernelGGL((k_row<T, IP, OFF, ROW_NUM, RowSmall>), dim3((unsigned)grid_for(n, RowSmall::WPB * ROW_PAIR)),
+                hipLaunchKernelGGL((k_row<T, IP, OFF, ROW_NUM, RowSmall>), dim3((unsigned)grid_for(n, RowSmall::WPB * row_pair<ROW_NUM>())),
                                    dim3(RowSmall::WPB * WAVE), 0, h->stream, r0, n, p.B.cols, Ap, Aj, Ax, Bp, Bj,
                                    Bx, off, cj, cx, alpha, p.row_cnt, l1, cnt, 0, (int64_t)0,
                                    (const int64_t*)nullptr, (unsigned long long*)nullptr, (int64_t)0,
@@ -857,7 +857,8 @@ spg_status_t alg1_fused_run(spg_handle_t h, spg_plan_s& p, void* cp) {
         // no memset of the control block: the count pass zeroes the scan's status words,
         // spills are counted in the handle's counter, which the scan moves into
         // scalars[5] and re-arms
-        const unsigned grid = (unsigned)grid_for(p.A.rows, RowSmall::WPB * ROW_PAIR);
+        const unsigned grid = (unsigned)grid_for(p.A.rows, RowSmall::WPB * row_pair<ROW_LB>());
+        const unsigned grid_sym = (unsigned)grid_for(p.A.rows, RowSmall::WPB * row_pair<ROW_SYM>());
         // the numeric launch's scan words: ticket + tile status, then the group prefixes
         unsigned long long* status = p.scan_status + scan_tiles(p.A.rows) + 1;
         const int64_t nscan = scan_tiles(p.A.rows);
@@ -867,7 +868,7 @@ spg_status_t alg1_fused_run(spg_handle_t h, spg_plan_s& p, void* cp) {
         if (!p.counts_ready) {
             if (h->spill_ctr_dirty) SPG_HIP(h, hipMemsetAsync(h->spill_ctr, 0, sizeof(int32_t), h->stream));
             h->spill_ctr_dirty = true;
-            timed_launch(h, SPG_PHASE_SYMBOLIC, k_row<double, IP, int64_t, ROW_SYM, RowSmall>, dim3(grid), dim3(RowSmall::WPB * WAVE),
+            timed_launch(h, SPG_PHASE_SYMBOLIC, k_row<double, IP, int64_t, ROW_SYM, RowSmall>, dim3(grid_sym), dim3(RowSmall::WPB * WAVE),
                                (int64_t)0, p.A.rows, p.B.cols, (const IP*)p.A.indptr,
                                (const int32_t*)p.A.indices, (const double*)nullptr, (const IP*)p.B.indptr,
                                (const int32_t*)p.B.indices, (const double*)nullptr, (const int64_t*)nullptr,

@@ -519,7 +519,14 @@ enum { ROW_COUNT_ALL = 1, ROW_LISTED = 2 };
 #ifndef SPG_ROW_PAIR
 #define SPG_ROW_PAIR 1
 #endif
-constexpr int ROW_PAIR = SPG_ROW_PAIR;   // rows per wave (k_row)
+#ifndef SPG_ROW_PAIR_SYM
+#define SPG_ROW_PAIR_SYM 1
+#endif
+// rows per wave, per mode.  Two rows per wave in the count pass (42 VGPRs, still 8 waves per
+// SIMD: config 2's 16384 rows become one generation of 8192 resident waves) measured no
+// gain (12.7 vs 12.1 us; three rows 15 us): the count pass is bound by its ~370 VALU
+// instructions per row, not by the dependent-load chain
+template <int MODE> constexpr int row_pair() { return MODE == 0 ? SPG_ROW_PAIR_SYM : SPG_ROW_PAIR; }
 // A's values re-read from LDS after the gathers instead of held in registers across them
 // (ROW_LB only): fewer live registers, but measured 1.5 us slower on config 2's numeric pass
 #ifndef SPG_ROW_AVLDS
@@ -540,6 +547,7 @@ __global__ __launch_bounds__(G::WPB * WAVE, sizeof(T) <= 8 ? 5 : 3) void k_row(
     constexpr bool VALS = MODE != ROW_SYM;
     constexpr bool lb = MODE == ROW_LB;
     constexpr bool AVL = lb && SPG_ROW_AVLDS;
+    constexpr int RP = row_pair<MODE>();
     __shared__ __attribute__((aligned(16))) RowLds<T, IP, G, VALS> lds[G::WPB];
     // (ALG1 count pass) the next launch's scan status words are zeroed here: no memset
     if (zero_words)
@@ -559,15 +567,15 @@ __global__ __launch_bounds__(G::WPB * WAVE, sizeof(T) <= 8 ? 5 : 3) void k_row(
     // ROW_PAIR consecutive rows per wave: both rows' fronts (A entries, B row extents) are
     // loaded before the first row is worked on, so the second row's dependent loads are
     // in flight during the first row's gathers and LDS work
-    const int64_t it0 = (((int64_t)blockIdx.x - (lb ? sa.nscan : 0)) * G::WPB + wv) * ROW_PAIR;
+    const int64_t it0 = (((int64_t)blockIdx.x - (lb ? sa.nscan : 0)) * G::WPB + wv) * RP;
     if (it0 >= nrows) return;
-    const int nr = (int)min((int64_t)ROW_PAIR, nrows - it0);
-    int64_t a0s[ROW_PAIR + 1];
+    const int nr = (int)min((int64_t)RP, nrows - it0);
+    int64_t a0s[RP + 1];
 #pragma unroll
-    for (int q = 0; q <= ROW_PAIR; ++q) a0s[q] = q <= nr ? (int64_t)Ap[row0 + it0 + q] : 0;
-    RowFront<T, IP> fr[ROW_PAIR];
+    for (int q = 0; q <= RP; ++q) a0s[q] = q <= nr ? (int64_t)Ap[row0 + it0 + q] : 0;
+    RowFront<T, IP> fr[RP];
 #pragma unroll
-    for (int q = 0; q < ROW_PAIR; ++q) {
+    for (int q = 0; q < RP; ++q) {
         const int nAq = q < nr ? (int)(a0s[q + 1] - a0s[q]) : 0;
         const bool f = nAq > 0 && nAq <= WAVE && ncols > 0;
         if (lb) {
@@ -578,11 +586,11 @@ __global__ __launch_bounds__(G::WPB * WAVE, sizeof(T) <= 8 ? 5 : 3) void k_row(
         }
     }
     // (lb) each row's group word and the counts of the rows before it in its group
-    unsigned long long gw[ROW_PAIR] = {};
-    int gc[ROW_PAIR] = {};   // (a row's count < 2^31: the low word of its int64 count)
+    unsigned long long gw[RP] = {};
+    int gc[RP] = {};   // (a row's count < 2^31: the low word of its int64 count)
     if (lb) {
 #pragma unroll
-        for (int q = 0; q < ROW_PAIR; ++q) {
+        for (int q = 0; q < RP; ++q) {
             gw[q] = 0;
             gc[q] = 0;
             if (q < nr) {
@@ -646,7 +654,7 @@ __global__ __launch_bounds__(G::WPB * WAVE, sizeof(T) <= 8 ? 5 : 3) void k_row(
         wsync();   // the next row reuses this wave's LDS
     };
 #pragma unroll
-    for (int q = 0; q < ROW_PAIR; ++q)
+    for (int q = 0; q < RP; ++q)
         if (q < nr) do_row(row0 + it0 + q, a0s[q], (int)(a0s[q + 1] - a0s[q]), fr[q], lb ? gw[q] : 0ull,
                            lb ? gc[q] : 0);
 }
