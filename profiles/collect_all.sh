@@ -4,7 +4,7 @@
 # one GPU (sparse tiles).  ROUND names the outputs.
 set -euo pipefail
 R=${ROUND:-r02}
-TAG=${R}_c2 PMC_KEY=c2_n16384_d0.001_float64_alg1_w1 PMC_KERNEL='k_row<double, int, int, 1' \
+TAG=${R}_c2 PMC_KEY=c2_n16384_d0.001_float64_alg1_w1 PMC_KERNEL='k_row<double, int, int, 2' \
     BENCH_ARGS="" bash profiles/collect.sh
 TAG=${R}_c4 PMC_KEY=c4_n65536_d0.005_float64_alg3_w1 PMC_KERNEL='k_tile<double, int, true' \
     BENCH_ARGS="--config 4 --steps 3 --warmup 1" bash profiles/collect.sh

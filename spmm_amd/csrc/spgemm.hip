@@ -567,17 +567,36 @@ spg_status_t plan_chunks(spg_handle_t h, spg_plan_s& p) {
     }
     p.P = hp[(size_t)rows];
     const int64_t cap = std::max<int64_t>(1, (int64_t)std::ceil((double)p.cf * (double)p.P));
-    p.chunk_rows.assign(1, 0);
-    p.chunk_nz.assign(1, ha[0]);
-    int64_t r = 0;
-    while (r < rows) {
-        // furthest row end e with pref[e] - pref[r] <= cap (at least one row)
-        const int64_t target = hp[(size_t)r] + cap;
-        int64_t e = (int64_t)(std::upper_bound(hp.begin() + r + 1, hp.end(), target) - hp.begin()) - 1;
-        if (e <= r) e = r + 1;
-        p.chunk_rows.push_back(e);
-        p.chunk_nz.push_back(ha[(size_t)e]);
-        r = e;
+    // n chunks of about equal products, n from ceil(P / cap) up: cut k lands on the row end
+    // nearest k*P/n such that chunk k stays within the cap and what is left still fits the
+    // remaining chunks.  Row ends rarely fall on k*P/n exactly, so chunk_fraction 0.2 gives
+    // six chunks of 16.7 % (a greedy fill to the cap gives 5 x 19.99 % + one tiny chunk).
+    // Rows longer than the slack fall back to the greedy fill (at least one row per chunk).
+    auto last_le = [&](int64_t r, int64_t v) {   // last row end e > r with pref[e] <= v (or r)
+        return (int64_t)(std::upper_bound(hp.begin() + r + 1, hp.end(), v) - hp.begin()) - 1;
+    };
+    int64_t n = std::max<int64_t>(1, (p.P + cap - 1) / cap);
+    for (int attempt = 0; attempt < 3; ++attempt, ++n) {
+        p.chunk_rows.assign(1, 0);
+        p.chunk_nz.assign(1, ha[0]);
+        int64_t r = 0;
+        for (int64_t k = 1; r < rows; ++k) {
+            int64_t e = last_le(r, hp[(size_t)r] + cap);   // the greedy bound
+            if (k < n && e < rows) {
+                const int64_t target = (int64_t)((long double)p.P * (long double)k / (long double)n);
+                const int64_t need = p.P - (n - k) * cap;   // pref[e] >= need: the rest fits
+                int64_t b = last_le(r, target);
+                if (b + 1 <= e && hp[(size_t)b + 1] - target < target - hp[(size_t)b]) ++b;
+                if (hp[(size_t)b] < need)
+                    b = std::min(e, (int64_t)(std::lower_bound(hp.begin() + r + 1, hp.end(), need) - hp.begin()));
+                e = std::min(e, b);
+            }
+            if (e <= r) e = r + 1;
+            p.chunk_rows.push_back(e);
+            p.chunk_nz.push_back(ha[(size_t)e]);
+            r = e;
+        }
+        if ((int64_t)p.chunk_rows.size() - 1 <= n) break;
     }
     int64_t mx = 0;
     for (size_t c = 0; c + 1 < p.chunk_nz.size(); ++c)
