@@ -61,6 +61,11 @@ __device__ __forceinline__ int wave_incl_sum(int v) {
     return v;
 }
 
+// lanes below this one whose bit of m is set
+__device__ __forceinline__ int lane_rank(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
+
 __device__ __forceinline__ long long wave_incl_sum64(long long v) {
     const int l = lane_id();
 #pragma unroll

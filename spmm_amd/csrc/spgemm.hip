@@ -461,6 +461,17 @@ inline int64_t tile_rows_max(const spg_plan_s& p) {
     return mx;
 }
 inline int64_t tile_items(const spg_plan_s& p) { return p.use_tile ? tile_rows_max(p) * p.G : 0; }
+// Dense numeric tiles (one accumulator window per tile) take an item's structure from the
+// accumulation itself: no symbolic bitmaps, and every item's 8-byte offset is kept (all
+// rows, not one chunk's), so ALG3's numeric phase does not recompute its chunks' counts.
+inline bool tile_dense(const spg_plan_s& p) {
+    return p.use_tile && (1 << p.tws) <= TILE_CAP && tile_variant().dense;
+}
+inline int64_t tile_item_slots(const spg_plan_s& p) { return tile_dense(p) ? p.A.rows * p.G : tile_items(p); }
+// item counts / offsets of chunk c (dense tiles: every chunk's stay, at its rows' place)
+inline int64_t* tile_chunk_items(const spg_plan_s& p, int64_t c) {
+    return tile_dense(p) ? p.item_cnt + tile_chunk_r0(p, c) * p.G : p.item_cnt;
+}
 inline int sym_tiles(const spg_plan_s& p) { const int R = 1 << (p.twss - p.tws); return (p.G + R - 1) / R; }
 inline int64_t bt_entries(const spg_plan_s& p) { return p.use_tile ? (int64_t)p.G * (p.B.rows + 1) : 0; }
 
@@ -494,10 +505,10 @@ Layout make_layout(const spg_plan_s& p) {
         L.tptr = off;  off = align_up(off + sizeof(int32_t) * (size_t)(bt_entries(p) + 1));
         L.sidx = off;  off = align_up(off + sizeof(uint32_t) * (size_t)p.B.rows * (size_t)(sym_tiles(p) + 1));
         L.brec = off;  off = align_up(off + brec_bytes(p.A.value_type) * (size_t)std::max<int64_t>(p.B.nnz, 1));
-        L.items = off; off = align_up(off + sizeof(int64_t) * (size_t)(tile_items(p) + 1));
+        L.items = off; off = align_up(off + sizeof(int64_t) * (size_t)(tile_item_slots(p) + 1));
         // item bitmaps; before the first symbolic pass the region holds the row-major
         // boundary index the tile-major B is built from
-        const size_t bm = sizeof(uint32_t) * (size_t)tile_items(p) * (size_t)((1 << p.tws) >> 5);
+        const size_t bm = tile_dense(p) ? 0 : sizeof(uint32_t) * (size_t)tile_items(p) * (size_t)((1 << p.tws) >> 5);
         const size_t ti = sizeof(uint2) * (size_t)p.B.rows * (size_t)p.G;
         L.bitmap = off; off = align_up(off + std::max(bm, ti));
     }
@@ -778,17 +789,18 @@ spg_status_t tile_build_index(spg_handle_t h, spg_plan_s& p) {
 template <typename IP>
 spg_status_t tile_sym_chunk(spg_handle_t h, spg_plan_s& p, int64_t c) {
     const int64_t r0 = tile_chunk_r0(p, c), n = tile_chunk_r1(p, c) - r0;
+    int64_t* items = tile_chunk_items(p, c);
     if (n > 0) {
         timed_launch(h, SPG_PHASE_SYMBOLIC, k_tile_sym<IP>, dim3(tile_grid(n * sym_tiles(p))), dim3(TILE_WPB * WAVE),
                            r0, n, p.tws, p.G, p.twss, (const IP*)p.A.indptr, (const int32_t*)p.A.indices,
-                           (const IP*)p.B.indptr, (const int32_t*)p.B.indices, (const uint32_t*)p.sidx, p.bitmap,
-                           p.item_cnt);
+                           (const IP*)p.B.indptr, (const int32_t*)p.B.indices, (const uint32_t*)p.sidx,
+                           tile_dense(p) ? (uint32_t*)nullptr : p.bitmap, items);
         SPG_LAUNCHED(h);
     }
     const int64_t nch = tile_chunks(p);
     int64_t* scal = c == nch - 1 ? p.scalars : p.scalars + 12 + 2 * (c & 1);
     const int64_t* seed = c == 0 ? nullptr : p.scalars + 12 + 2 * ((c - 1) & 1);
-    return launch_scan<int64_t>(h, n * p.G, (const int64_t*)p.item_cnt, p.item_cnt, item_scan_status(p), scal,
+    return launch_scan<int64_t>(h, n * p.G, (const int64_t*)items, items, item_scan_status(p), scal,
                                 true, nullptr, nullptr, nullptr, 0, 0, seed);
 }
 
@@ -796,20 +808,25 @@ template <typename OUT>
 spg_status_t tile_rowptr_chunk(spg_handle_t h, spg_plan_s& p, int64_t c, void* cp) {
     const int64_t r0 = tile_chunk_r0(p, c), n = tile_chunk_r1(p, c) - r0;
     timed_launch(h, SPG_PHASE_SCAN, k_items_to_rowptr<OUT>, dim3((unsigned)grid_for(n + 1, 256)), dim3(256), n, p.G,
-                 (const int64_t*)p.item_cnt, (OUT*)cp + r0);
+                 (const int64_t*)tile_chunk_items(p, c), (OUT*)cp + r0);
     SPG_LAUNCHED(h);
     return SPG_STATUS_SUCCESS;
 }
 
 // spg_symbolic on the tile path: every chunk's counts, offsets and row pointer.  A single
-// chunk's offsets stay valid for the numeric pass (and a repeated call only rewrites the
-// row pointer); with several chunks the numeric pass recomputes each chunk's.
+// chunk's offsets -- every chunk's on dense tiles -- stay valid for the numeric pass (and a
+// repeated call only rewrites the row pointer); otherwise the numeric pass recomputes each
+// chunk's.
 template <typename IP, typename OUT>
 spg_status_t tile_symbolic(spg_handle_t h, spg_plan_s& p, void* cp) {
     spg_status_t st;
     if ((st = tile_build_index<IP>(h, p))) return st;
     const int64_t nch = tile_chunks(p);
-    if (nch == 1 && p.counts_ready) return tile_rowptr_chunk<OUT>(h, p, 0, cp);
+    if ((nch == 1 || tile_dense(p)) && p.counts_ready) {
+        for (int64_t c = 0; c < nch; ++c)
+            if ((st = tile_rowptr_chunk<OUT>(h, p, c, cp))) return st;
+        return SPG_STATUS_SUCCESS;
+    }
     for (int64_t c = 0; c < nch; ++c) {
         if ((st = tile_sym_chunk<IP>(h, p, c))) return st;
         if ((st = tile_rowptr_chunk<OUT>(h, p, c, cp))) return st;
@@ -818,7 +835,8 @@ spg_status_t tile_symbolic(spg_handle_t h, spg_plan_s& p, void* cp) {
 }
 
 // spg_numeric on the tile path: the tile-major B records once, then chunk by chunk (the
-// chunk's counts, bitmaps and offsets again when there are several) the numeric tiles.
+// chunk's counts, bitmaps and offsets again when there are several and the tiles are not
+// dense) the numeric tiles.
 template <typename T, typename IP>
 spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T alpha) {
     const IP* Ap = (const IP*)p.A.indptr;
@@ -836,20 +854,21 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
     const int64_t nch = tile_chunks(p);
     for (int64_t c = 0; c < nch; ++c) {
         spg_status_t st;
-        if (nch > 1 && (st = tile_sym_chunk<IP>(h, p, c))) return st;
+        if (nch > 1 && !tile_dense(p) && (st = tile_sym_chunk<IP>(h, p, c))) return st;
         const int64_t r0 = tile_chunk_r0(p, c), n = tile_chunk_r1(p, c) - r0;
         if (n <= 0) continue;
         KernelTimer kt(h, SPG_PHASE_NUMERIC);
         // dense accumulator when the tile fits one window; round groups (tile_variant())
-        const bool dense = (1 << p.tws) <= TILE_CAP && tile_variant().dense;
+        const bool dense = tile_dense(p);
         const int ru = tile_variant().ru;
         auto launch = [&](auto dn, auto rn) {
             constexpr bool DN = decltype(dn)::value;
             constexpr int RN = decltype(rn)::value;
             hipExtLaunchKernelGGL((k_tile<T, IP, DN, RN>), dim3(tile_grid(n * p.G)), dim3(TILE_WPB * WAVE), 0,
                                   h->stream, kt.a, kt.b, 0, r0, n, p.tws, p.G, Ap, Aj, Ax, p.B.rows,
-                                  (const uint32_t*)p.brec, (const int32_t*)p.tptr, (const uint32_t*)p.bitmap,
-                                  (const int64_t*)p.item_cnt, cj, cx, alpha, tile_variant().diag);
+                                  (const uint32_t*)p.brec, (const int32_t*)p.tptr,
+                                  dense ? (const uint32_t*)nullptr : (const uint32_t*)p.bitmap,
+                                  (const int64_t*)tile_chunk_items(p, c), cj, cx, alpha, tile_variant().diag);
         };
         constexpr int UF = sizeof(T) > 8 ? 4 : 8;
         using D1 = std::integral_constant<bool, true>;

@@ -98,9 +98,6 @@ template <typename T> __device__ __forceinline__ T readlane_v(T v, int j) {
     return r;
 }
 
-__device__ __forceinline__ int lane_rank(unsigned long long m) {
-    return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-}
 
 template <typename T> __device__ __forceinline__ T scale(T alpha, T v) {
     return alpha == (T)1 ? v : mul_rn(alpha, v);

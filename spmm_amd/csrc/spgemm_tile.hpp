@@ -320,8 +320,10 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile_sym(
             }
         }
         wsync();
-        uint32_t* __restrict__ out = bitmap + ((row - row0) * G + t0) * (int64_t)nw;
-        for (int w = l; w < nws; w += WAVE) out[w] = S.bits[w];
+        if (bitmap) {   // (dense numeric tiles take their structure from the accumulation)
+            uint32_t* __restrict__ out = bitmap + ((row - row0) * G + t0) * (int64_t)nw;
+            for (int w = l; w < nws; w += WAVE) out[w] = S.bits[w];
+        }
         // entry count of each numeric tile: lane t sums tile t's words (rotated start: no
         // two lanes read one bank together)
         for (int t = l; t < t1 - t0; t += WAVE) {
@@ -376,32 +378,40 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile(
         const int64_t a0 = Ap[row];
         const int nA = (int)(Ap[row + 1] - a0);
         if (nA <= 0) continue;
-        const uint32_t* __restrict__ ibits = bitmap + item * nw;
-        // the symbolic bitmap and its popcount prefix (lane owns wpl words)
+        // the item's entries: DENSE from its offsets (its structure comes from the
+        // accumulation tags below); otherwise the symbolic bitmap and its popcount prefix
+        // (lane owns wpl words)
         const int w0 = min(nw, l * wpl), w1 = min(nw, w0 + wpl);
-        uint32_t wd[2] = {0u, 0u};
-        int mine = 0;
-#pragma unroll
-        for (int q = 0; q < 2; ++q)
-            if (w0 + q < w1) {
-                wd[q] = ibits[w0 + q];
-                mine += __popc(wd[q]);
-            }
-        const int pincl = wave_incl_sum_dpp(mine);
-        const int nnz = readlane_i(pincl, WAVE - 1);
-        if (nnz == 0) continue;
-        const int p0 = pincl - mine;
-        wsync();
-        {
-            int run = p0;
+        int nnz, pincl = 0, p0 = 0;
+        if constexpr (DENSE) {
+            nnz = (int)(item_off[item + 1] - item_off[item]);
+            if (nnz == 0) continue;
+        } else {
+            const uint32_t* __restrict__ ibits = bitmap + item * nw;
+            uint32_t wd[2] = {0u, 0u};
+            int mine = 0;
 #pragma unroll
             for (int q = 0; q < 2; ++q)
                 if (w0 + q < w1) {
-                    S.bw[w0 + q] = make_uint2(wd[q], (uint32_t)run);
-                    run += __popc(wd[q]);
+                    wd[q] = ibits[w0 + q];
+                    mine += __popc(wd[q]);
                 }
+            pincl = wave_incl_sum_dpp(mine);
+            nnz = readlane_i(pincl, WAVE - 1);
+            if (nnz == 0) continue;
+            p0 = pincl - mine;
+            wsync();
+            {
+                int run = p0;
+#pragma unroll
+                for (int q = 0; q < 2; ++q)
+                    if (w0 + q < w1) {
+                        S.bw[w0 + q] = make_uint2(wd[q], (uint32_t)run);
+                        run += __popc(wd[q]);
+                    }
+            }
+            wsync();
         }
-        wsync();
         const int64_t obase = item_off[item];
         // The first NB batches of A entries (rows of <= NB*64 entries: all of them): every
         // lane's A entry, value and tile segment, loaded at once up front (two dependent
@@ -472,7 +482,10 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile(
                 }
             }
             wsync();
-            uint32_t seq = 0x7fffffu;   // 23 bits: key = seq | chunk (3 bits) | lane (6 bits)
+            // 23 bits: key = seq | chunk (3 bits) | lane (6 bits); every key < 0xfffffdff, so
+            // a tag below 0xfffffffe marks a column some product reached (DENSE: the
+            // item's structure)
+            uint32_t seq = 0x7ffffeu;
             for (int b = 0; b < ((diag & 4) ? 0 : nA); b += WAVE) {   // (diag 4, timing only: no batches)
                 int cnt, off, Pb;
                 batch(b, cnt, off, Pb);
@@ -568,10 +581,11 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile(
                         if (nu > 3 * U / 4) step(std::integral_constant<int, U>{});
                         else if (nu > U / 2) step(std::integral_constant<int, 3 * U / 4>{});
                         else step(std::integral_constant<int, U / 2>{});
-                        if (seq < 4096u) {   // re-arm the tag space (very long items only)
-                            wsync();
-                            for (int p = l; p < span; p += WAVE) S.tag[p] = 0xffffffffu;
-                            seq = 0x7fffffu;
+                        if (seq < 4096u) {   // re-arm the tag space (very long items only), keeping
+                            wsync();          // which columns were reached (0xfffffffe)
+                            for (int p = l; p < span; p += WAVE)
+                                S.tag[p] = S.tag[p] == 0xffffffffu ? 0xffffffffu : 0xfffffffeu;
+                            seq = 0x7ffffeu;
                             wsync();
                         }
                     }
@@ -579,22 +593,23 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile(
             }
             wsync();
             if constexpr (DENSE) {
-                // every set bit of the tile's bitmap, in column order: lane l looks at bit
-                // l % 32 of word 2i + l / 32; its output position is the word's prefix plus
-                // the bits below it
+                // the item's structure from the tags, 64 columns at a time: lane l looks at
+                // column 64k + l; a column some product reached is an entry, its output
+                // position the entries before it (the ballot's lower lanes plus the run)
                 int32_t* __restrict__ crow = Cj + obase;
                 T* __restrict__ xrow = Cx + obase;
-                for (int wq = 0; wq < nw; wq += 2) {
-                    const int w = wq + (l >> 5), bt = l & 31;
-                    if (w < nw) {
-                        const uint2 bw = S.bw[w];
-                        if (((bw.x >> bt) & 1u) && !(diag & 8)) {   // (diag 8, timing only: no output)
-                            const int p = (int)bw.y + __popc(bw.x & ((1u << bt) - 1u));
-                            crow[p] = lo + 32 * w + bt;
-                            const T val = S.acc[32 * w + bt];
-                            xrow[p] = (alpha == (T)1) ? val : mul_rn(alpha, val);
-                        }
+                int run = 0;
+                for (int k = 0; k < TW / WAVE; ++k) {
+                    const int c = k * WAVE + l;
+                    const bool hit = S.tag[c] != 0xffffffffu;
+                    const unsigned long long m = __ballot(hit);
+                    if (hit && !(diag & 8)) {   // (diag 8, timing only: no output)
+                        const int p = run + lane_rank(m);
+                        crow[p] = lo + c;
+                        const T val = S.acc[c];
+                        xrow[p] = (alpha == (T)1) ? val : mul_rn(alpha, val);
                     }
+                    run += (int)__popcll(m);
                 }
                 wsync();
                 break;

@@ -11,8 +11,8 @@
   B row lengths.
 * Config 5 on one GPU (N = 262144, density 1e-3, ALG2): the same checks (200 GB of C and
   workspace fit the 288 GB of one MI355X).
-* ALG3's working-set cap on a tile-path shape: peak bytes fall as chunk_fraction falls,
-  with bit-identical results.
+* ALG3's working-set cap on a sparse-tile shape: peak bytes fall as chunk_fraction falls,
+  with bit-identical results; on dense tiles ALG3 stays within ALG2's peak.
 
 Inputs of configs 4/5 are generated on the device (spmm_amd.gen.random_csr); the oracle
 sees only the sampled rows of A (and all of B).
@@ -131,12 +131,13 @@ def test_large_config_sampled_and_properties(n, density, alg, cf, expect_product
 
 
 def test_alg3_peak_falls_with_chunk_fraction():
-    """ALG3 caps the tile path's working set (items and bitmaps sized by the largest chunk,
-    reused chunk by chunk): peak bytes fall as chunk_fraction falls, the result does not
-    change (the reference's alg3.cu:195-202 / BASELINE.md 1a behaviour)."""
+    """ALG3 caps the tile path's working set where it has one: on sparse tiles (4096-column
+    tiles, compact windows) the symbolic bitmaps are sized by the largest chunk and reused
+    chunk by chunk, so peak bytes fall as chunk_fraction falls, the result does not change
+    (the reference's alg3.cu:195-202 / BASELINE.md 1a behaviour)."""
     from spmm_amd import cusparse, gen
     from spmm_amd.sparse import csr_matrix
-    Ah, Bh = gen.scipy_pair(8192, 1e-2, seed=42)
+    Ah, Bh = gen.scipy_pair(32768, 1e-3, seed=42)
     A, B = csr_matrix(Ah, device=DEV), csr_matrix(Bh, device=DEV)
     peaks, ref = [], None
     for cf in (1.0, 0.2, 0.05):
@@ -153,3 +154,28 @@ def test_alg3_peak_falls_with_chunk_fraction():
     # cf=0.05 (what stays is the tile-major copy of B, independent of cf)
     c_bytes = 12 * len(ref[1]) + 4 * len(ref[0])
     assert (peaks[2] - c_bytes) * 1.5 <= (peaks[0] - c_bytes), (peaks, c_bytes)
+    rp, rj, rx = oracle.spgemm(Ah[:512], Bh, keep_zeros=True, sort=True)
+    assert np.array_equal(ref[0][:513].astype(np.int64), rp) and np.array_equal(ref[1][:rp[-1]], rj)
+    assert np.array_equal(ref[2][:rp[-1]], _bits(rx))
+
+
+def test_alg3_dense_tiles_within_alg2_peak():
+    """On dense tiles (<= 1024 columns: config 4's shape) an item keeps only its 8-byte
+    offset -- the numeric tiles take the structure from their accumulation -- so there is
+    no per-chunk working set left to cap: every chunk_fraction gives the same C as ALG2,
+    at no more memory, without recomputing the chunks' counts."""
+    from spmm_amd import cusparse, gen
+    from spmm_amd.sparse import csr_matrix
+    Ah, Bh = gen.scipy_pair(8192, 1e-2, seed=42)
+    A, B = csr_matrix(Ah, device=DEV), csr_matrix(Bh, device=DEV)
+    C2 = cusparse.spgemm(A, B, alg=2)
+    torch.cuda.synchronize()
+    peak2 = cusparse.last_stats.peak_bytes
+    ref = (C2.indptr.cpu().numpy(), C2.indices.cpu().numpy(), _bits(C2.data.cpu().numpy()))
+    del C2
+    for cf in (1.0, 0.2, 0.05):
+        C = cusparse.spgemm(A, B, alg=3, chunk_fraction=cf)
+        torch.cuda.synchronize()
+        assert cusparse.last_stats.peak_bytes <= peak2 * 1.01, (cf, cusparse.last_stats.peak_bytes, peak2)
+        got = (C.indptr.cpu().numpy(), C.indices.cpu().numpy(), _bits(C.data.cpu().numpy()))
+        assert all(np.array_equal(x, y) for x, y in zip(got, ref)), f"cf={cf} changed C"
