@@ -118,9 +118,10 @@ def cpu_baseline(A_h, B_h, rows_sample, budget_s):
             "host_cpus": os.cpu_count()}
 
 
-def traffic_for(pmc_path, key, build_id):
+def traffic_for(pmc_path, key, build_id, source_id=None):
     """HBM bytes per launch from the committed PMC summary -- only when it was collected on
-    this very build of the library (else None: the number would be stale)."""
+    this very build of the library, or on a build of the same sources (else None: the
+    number would be stale)."""
     if not os.path.exists(pmc_path):
         return None, None
     try:
@@ -128,7 +129,7 @@ def traffic_for(pmc_path, key, build_id):
             e = json.load(f).get(key, {})
     except Exception:
         return None, None
-    if e.get("build_id") != build_id:
+    if e.get("build_id") != build_id and (source_id is None or e.get("source_id") != source_id):
         return None, e.get("build_id")
     return e.get("hbm_bytes_per_launch"), e.get("build_id")
 
@@ -281,7 +282,7 @@ def main():
     bytes_launch = bytes_product / launches_per_product
     achieved = bytes_launch / (avg_num_ms * 1e-3) / 1e9
     key = f"c{cfg_name}_n{n}_d{dens:g}_{args.dtype}_alg{alg}_w{world}"
-    traffic, traffic_build = traffic_for(args.pmc, key, _lib.build_id())
+    traffic, traffic_build = traffic_for(args.pmc, key, _lib.build_id(), _lib.source_id())
 
     # ---- CPU baseline (rank 0 at N=1): scipy A@B, the reference's comparator
     cpu = None

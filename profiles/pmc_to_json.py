@@ -42,7 +42,7 @@ def per_launch(d, counter, rx):
 
 
 def main():
-    from spmm_amd._lib import build_id
+    from spmm_amd._lib import build_id, source_id
     d, key, pat = sys.argv[1], sys.argv[2], sys.argv[3]
     path = sys.argv[4] if len(sys.argv) > 4 else os.path.join(os.path.dirname(__file__), "pmc_traffic.json")
     rx = re.compile(pat)
@@ -58,7 +58,7 @@ def main():
                "read_bytes_per_launch": int(rd), "write_bytes_per_launch": int(wr),
                "hbm_bytes_per_launch": int(rd + wr),
                "note": "FETCH_SIZE x2 (gfx950) + WRITE_SIZE; Infinity-Cache hits included",
-               "build_id": build_id()}
+               "build_id": build_id(), "source_id": source_id()}
     json.dump(db, open(path, "w"), indent=1, sort_keys=True)
     print(json.dumps({key: db[key]}))
 

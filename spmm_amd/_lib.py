@@ -136,6 +136,34 @@ def build_id() -> str:
     return _build_id
 
 
+_source_id = None
+
+
+def source_id() -> str:
+    """First 16 hex digits of the SHA-256 of the sources the library is compiled from
+    (spmm_amd/csrc/*.hip, *.hpp, include/*.h, the Makefile's flags).  hipcc's output is not
+    byte-identical from one build to the next, so a rebuild of the same sources changes
+    build_id() but not this; measurements carry both."""
+    global _source_id
+    if _source_id is None:
+        import glob
+        import hashlib
+        root = os.path.dirname(_HERE)
+        files = sorted(glob.glob(os.path.join(_HERE, "csrc", "*.hip")) + glob.glob(os.path.join(_HERE, "csrc", "*.hpp"))
+                       + glob.glob(os.path.join(root, "include", "*.h")))
+        h = hashlib.sha256()
+        for fn in files:
+            h.update(os.path.basename(fn).encode())
+            with open(fn, "rb") as f:
+                h.update(f.read())
+        mk = os.path.join(root, "Makefile")
+        if os.path.exists(mk):
+            with open(mk) as f:
+                h.update("".join(l for l in f if l.startswith(("HIPFLAGS", "ARCH"))).encode())
+        _source_id = h.hexdigest()[:16]
+    return _source_id
+
+
 def check(status: int, where: str = "") -> None:
     if status != 0:
         raise SpgError(status, where)
