@@ -32,19 +32,37 @@ template <typename T, typename IP, bool VALS> struct TileLds {
 };
 
 // Numeric tile pass LDS: the bitmap word and its popcount prefix side by side (one 8-byte
-// read per product), the A-entry table as one 16-byte entry per lane.
-template <typename T, typename IP> struct __attribute__((aligned(16))) TileEnt {
+// read per product; sparse tiles only), the A-entry table as one 8-byte entry per lane (the
+// A values stay in registers and reach the product lanes by a lane shuffle), the markers
+// of 8 chunks.  Dense tiles thus take 13 KB per wave: 12 waves per CU (6 blocks of 2)
+// instead of 10 at 15 KB.
+constexpr int NUM_MK = 512;   // numeric marker bytes: 8 chunks of 64 products per group
+template <typename IP> struct __attribute__((aligned(8))) TileSeg {
     IP jb0;          // first B index of the entry's segment
     uint32_t joff;   // flattened offset of the segment's first product
-    T ja;            // the A value
 };
-template <typename T, typename IP> struct NumLds {
-    uint2 bw[TILE_NWMAX];   // (bitmap word, popcount prefix)
+template <typename T, typename IP, bool DENSE> struct NumLds {
+    uint2 bw[DENSE ? 1 : TILE_NWMAX];   // (bitmap word, popcount prefix)
     T acc[TILE_CAP];
     uint32_t tag[TILE_CAP];
-    TileEnt<T, IP> ent[WAVE];
-    uint8_t mk[TILE_MK];
+    TileSeg<IP> ent[WAVE];
+    uint8_t mk[NUM_MK];
 };
+
+// Numeric lane -> A-entry markers for a group of up to 8 chunks (512 products) starting at
+// gbase, transposed as in group_markers: product t's marker at byte 8 * (t % 64) + t / 64,
+// so each lane reads all 8 of its chunks' markers with one 8-byte LDS load.
+template <typename L>
+__device__ __forceinline__ void num_group_markers(L& S, int l, int cnt, int off, int gbase) {
+    wsync();
+    reinterpret_cast<uint2*>(S.mk)[l] = make_uint2(0u, 0u);
+    wsync();
+    if (cnt > 0 && off >= gbase && off < gbase + NUM_MK) {
+        const int t = off - gbase;
+        S.mk[((t & (WAVE - 1)) << 3) | (t >> 6)] = (uint8_t)(l + 1);
+    }
+    wsync();
+}
 
 // ---------------------------------------------------------------------------------------
 // B column-tile index: tidx[k*G + g] = (start, end) of B row k's entries with columns in
@@ -361,10 +379,10 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile(
     int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha, int diag) {
     constexpr int U = sizeof(T) > 8 ? 4 : 8;   // chunks in flight (complex128: half)
     static_assert(U % RU == 0, "round groups split the chunks in flight");
-    __shared__ __attribute__((aligned(16))) NumLds<T, IP> lds[TILE_WPB];
+    __shared__ __attribute__((aligned(16))) NumLds<T, IP, DENSE> lds[TILE_WPB];
     const int l = lane_id();
     const int wv = uniform((int)(threadIdx.x >> 6));
-    NumLds<T, IP>& S = lds[wv];
+    NumLds<T, IP, DENSE>& S = lds[wv];
     const int TW = 1 << tws;
     const int nw = TW >> 5;                    // bitmap words of a tile
     const int wpl = (nw + WAVE - 1) / WAVE;    // words per lane (<= 2)
@@ -435,7 +453,7 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile(
             if (kq[q] >= 0) sq[q] = seg_pair(tp, kq[q]);
         }
         // lane info of one batch of A entries: (first B index, count) of its tile segment
-        auto batch = [&](int b, int& cnt, int& off, int& Pb) {
+        auto batch = [&](int b, int& cnt, int& off, int& Pb, T& bav) {
             cnt = 0;
             IP beg = 0;
             T av = (T)0;
@@ -457,7 +475,8 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile(
             off = incl - cnt;
             Pb = readlane_i(incl, WAVE - 1);
             wsync();
-            S.ent[l] = TileEnt<T, IP>{beg, (uint32_t)off, av};
+            S.ent[l] = TileSeg<IP>{beg, (uint32_t)off};
+            bav = av;
             wsync();
         };
         for (int L0 = 0; L0 < WAVE;) {
@@ -488,12 +507,14 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile(
             uint32_t seq = 0x7ffffeu;
             for (int b = 0; b < ((diag & 4) ? 0 : nA); b += WAVE) {   // (diag 4, timing only: no batches)
                 int cnt, off, Pb;
-                batch(b, cnt, off, Pb);
+                T bav;   // this lane's A value of the batch
+                batch(b, cnt, off, Pb, bav);
                 unsigned carry = 0u;
-                for (int gb = 0; gb < Pb; gb += TILE_MK) {
-                    group_markers(S, l, cnt, off, gb);
-                    const int nchg = min(TILE_MK, Pb - gb);
-                    const uint4 mrow = reinterpret_cast<const uint4*>(S.mk)[l];
+                for (int gb = 0; gb < Pb; gb += NUM_MK) {
+                    num_group_markers(S, l, cnt, off, gb);
+                    const int nchg = min(NUM_MK, Pb - gb);
+                    const uint2 m2 = reinterpret_cast<const uint2*>(S.mk)[l];
+                    const uint64_t mrow = ((uint64_t)m2.y << 32) | m2.x;
                     for (int c0 = 0; c0 < nchg; c0 += U * WAVE) {
                         // U, 3U/4 or U/2 chunks at once, the fewest that hold the group's
                         // remaining products (a wave-uniform choice: short batches scan and
@@ -504,7 +525,7 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile(
                             constexpr int RG = RU < NU ? RU : NU;
                             // NU chunks at once (nu of them hold products: a wave-uniform count):
                             // the lane -> A entry scans, then every record load in flight.
-                            const uint64_t mb = marker_bytes(mrow, c0 >> 6);
+                            const uint64_t mb = mrow >> (8 * (c0 >> 6));
                             // (slots past nu scan zero markers and load record 0: no branches
                             // between the loads, so they all stay in flight)
                             unsigned sp[NU];
@@ -522,9 +543,10 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile(
                             for (int u = 0; u < NU; ++u) {
                                 const int t = gb + c0 + u * WAVE + l;
                                 val[u] = u < nu && t < Pb;
-                                const TileEnt<T, IP> e = S.ent[(int)max(sp[u], 1u) - 1];
+                                const int src = (int)max(sp[u], 1u) - 1;
+                                const TileSeg<IP> e = S.ent[src];
                                 idx[u] = val[u] ? e.jb0 + (IP)(t - (int)e.joff) : (IP)0;
-                                av[u] = e.ja;
+                                av[u] = shfl_v(bav, src);
                             }
                             int qc[NU];
                             T qv[NU];
