@@ -202,8 +202,8 @@ inline bool want_tile(const spg_csr_t& A, const spg_csr_t& B, int& tws, int& G) 
 }
 
 // grid of a tile kernel over `tasks` wave tasks: a multiple of 8 (XCD-aware block ids)
-inline unsigned tile_grid(int64_t tasks) {
-    const int64_t nb = std::max<int64_t>(1, std::min<int64_t>(grid_for(tasks, TILE_WPB), 1 << 26));
+inline unsigned tile_grid(int64_t tasks, int wpb = TILE_WPB) {
+    const int64_t nb = std::max<int64_t>(1, std::min<int64_t>(grid_for(tasks, wpb), 1 << 26));
     return (unsigned)((nb + 7) / 8 * 8);
 }
 
@@ -864,7 +864,8 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
         auto launch = [&](auto dn, auto rn) {
             constexpr bool DN = decltype(dn)::value;
             constexpr int RN = decltype(rn)::value;
-            hipExtLaunchKernelGGL((k_tile<T, IP, DN, RN>), dim3(tile_grid(n * p.G)), dim3(TILE_WPB * WAVE), 0,
+            constexpr int WPBN = tile_num_wpb<DN>();
+            hipExtLaunchKernelGGL((k_tile<T, IP, DN, RN>), dim3(tile_grid(n * p.G, WPBN)), dim3(WPBN * WAVE), 0,
                                   h->stream, kt.a, kt.b, 0, r0, n, p.tws, p.G, Ap, Aj, Ax, p.B.rows,
                                   (const uint32_t*)p.brec, (const int32_t*)p.tptr,
                                   dense ? (const uint32_t*)nullptr : (const uint32_t*)p.bitmap,

@@ -16,6 +16,9 @@
 namespace spg {
 
 constexpr int TILE_WPB = 2;           // waves per block
+// waves per block of the numeric kernel: sparse tiles (14 KB of LDS per wave) fit 11
+// one-wave blocks per CU where 2-wave blocks fit 10; dense tiles (13 KB) fit 12 either way
+template <bool DENSE> constexpr int tile_num_wpb() { return DENSE ? 2 : 1; }
 constexpr int TILE_CAP = 1024;        // entries per window
 constexpr int TILE_NWMAX = 128;       // bitmap words per tile: TW <= 4096 columns
 constexpr int TILE_MK = 1024;         // marker bytes: 16 chunks of 64 products per group
@@ -371,7 +374,7 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile_sym(
 // the next (smaller) round number.  Within a group the lowest (chunk, lane) -- the earliest
 // product in flattened order -- of every position adds first; groups run in order.
 template <typename T, typename IP, bool DENSE, int RU>
-__global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile(
+__global__ __launch_bounds__(tile_num_wpb<DENSE>() * WAVE) void k_tile(
     int64_t row0, int64_t nrows, int tws, int G, const IP* __restrict__ Ap,
     const int32_t* __restrict__ Aj, const T* __restrict__ Ax, int64_t K,
     const uint32_t* __restrict__ brec, const int32_t* __restrict__ tptr,
@@ -379,7 +382,8 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile(
     int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha, int diag) {
     constexpr int U = sizeof(T) > 8 ? 4 : 8;   // chunks in flight (complex128: half)
     static_assert(U % RU == 0, "round groups split the chunks in flight");
-    __shared__ __attribute__((aligned(16))) NumLds<T, IP, DENSE> lds[TILE_WPB];
+    constexpr int WPB = tile_num_wpb<DENSE>();
+    __shared__ __attribute__((aligned(16))) NumLds<T, IP, DENSE> lds[WPB];
     const int l = lane_id();
     const int wv = uniform((int)(threadIdx.x >> 6));
     NumLds<T, IP, DENSE>& S = lds[wv];
@@ -387,7 +391,7 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile(
     const int nw = TW >> 5;                    // bitmap words of a tile
     const int wpl = (nw + WAVE - 1) / WAVE;    // words per lane (<= 2)
     const uint32_t items = (uint32_t)(nrows * G);   // host keeps rows*G < 2^31
-    for (uint32_t it = xcd_block(gridDim.x) * TILE_WPB + wv; it < items; it += gridDim.x * TILE_WPB) {
+    for (uint32_t it = xcd_block(gridDim.x) * WPB + wv; it < items; it += gridDim.x * WPB) {
         const int g = (int)(it / (uint32_t)nrows);
         const int64_t row = row0 + (int64_t)(it - (uint32_t)g * (uint32_t)nrows);
         const int64_t item = (row - row0) * G + g;   // items (and bitmaps) of this chunk of rows
