@@ -12,6 +12,7 @@ OUT=$PWD/gpurun_out
 P=$OUT/prof_$TAG
 mkdir -p "$P"
 export TMPDIR=/tmp
+# (the box starts without gpurun_out: take the committed file, keep every other entry)
 [ -f "$OUT/pmc_traffic.json" ] || cp profiles/pmc_traffic.json "$OUT/pmc_traffic.json"
 timeout -k 10 400 python bench.py $ARGS > "$OUT/bench_$TAG.json" 2> "$OUT/bench_$TAG.err"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$P" -o trace \
