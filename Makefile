@@ -22,9 +22,12 @@ fastpath: $(FASTPATH)
 $(FASTPATH): spmm_amd/csrc/fastpath.cpp include/spgemm.h spmm_amd/build_fastpath.py $(LIB)
 	python3 spmm_amd/build_fastpath.py
 
-$(LIB): $(SRC) $(HDRS)
+# the source id (sources + effective HIPFLAGS) is compiled into the library: spg_build_info()
+$(LIB): $(SRC) $(HDRS) spmm_amd/source_id.py
 	@mkdir -p $(dir $@)
-	$(HIPCC) $(HIPFLAGS) -shared -Wl,-soname,libmi355_spgemm.so -Iinclude -Ispmm_amd/csrc $(SRC) -o $@
+	$(HIPCC) $(HIPFLAGS) -DSPG_SOURCE_ID='"$(shell python3 spmm_amd/source_id.py '$(HIPFLAGS)')"' \
+	    -DSPG_HIPFLAGS='"$(strip $(HIPFLAGS))"' -shared -Wl,-soname,libmi355_spgemm.so -Iinclude -Ispmm_amd/csrc \
+	    $(SRC) -o $@
 
 # the three reference driver names, one source; ALG fixed at compile time
 drivers/bin/spgemm_from_txt_alg%: drivers/spgemm_from_txt.cpp include/spgemm.h $(LIB)

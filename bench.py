@@ -4,32 +4,47 @@
 Step = one complete ``C = A.B`` through the drop-in shim (``spmm_amd.cusparse.spgemm``:
 plan, symbolic with its nnz(C) host sync, C allocation, numeric), inputs resident in HBM.
 
-Workloads (``--config``; ``auto`` = 2 on one GPU, 5 on several):
+Workloads (``--config``; ``auto`` = 4 at every N):
 
-* ``2`` (N=1 default, BASELINE configs[1]): random 16384 x 16384, density 1e-3, fp64, A then
-  B from one ``default_rng(42)`` stream via scipy.sparse.random (nnz(C) = 4,366,124,
-  P = 4,402,284), ALG1 single pass.
-* ``4``: N = 65536, density 5e-3, fp64, ALG3 chunked (chunk_fraction 0.2): nnz(C) = 3.46e9,
-  int64 row pointer.  Inputs generated on the device (spmm_amd.gen.random_csr).
-* ``5``: N = 262144, density 1e-3, fp64, ALG2, strong scaling over the ranks: rank r owns
-  the rows [r0, r1) cut on the product-count prefix, B (826 MB) is broadcast from rank 0
-  over RCCL/xGMI INSIDE every step -- structure first, values in flight while the
-  symbolic pass runs (spmm_amd.distributed.rowblock_step) -- and every rank writes its own
-  C slab: no reduction.  value = sum_r 2 P_r per step / max-over-ranks step time.  At
-  ``--gpus 1`` it is the whole problem on one GPU (200 GB of C and workspace fit in 288 GB).
+* ``4`` (the N=1 headline: the largest single-GPU configuration of BASELINE.json, configs[3]):
+  N = 65536, density 5e-3, fp64, ALG3 chunked (chunk_fraction 0.2) -- the reference's ALG3
+  path, estimateMemory then a chunked compute (cupy_cusparse/spgemm_from_txt_alg3.cu:194-208).
+  nnz(C) = 3.46e9: int64 row pointer.  Inputs generated on the device (spmm_amd.gen.random_csr).
+  At N > 1 it scales WEAK: rank r owns rows [r*65536, (r+1)*65536) of an (N*65536) x 65536
+  A of the same density (rank 0's block is the N=1 A), B (258 MB) is broadcast from rank 0
+  over RCCL/xGMI inside every step -- structure first, values in flight while the symbolic
+  pass runs (spmm_amd.distributed.rowblock_step) -- and every rank writes its own C slab: no
+  reduction.  value = sum_r 2 P_r / max-over-ranks time.
+* ``2`` (BASELINE configs[1]): random 16384 x 16384, density 1e-3, fp64, A then B from one
+  ``default_rng(42)`` stream via scipy.sparse.random (nnz(C) = 4,366,124, P = 4,402,284), ALG1
+  single pass.  Reported as the ``config2`` key of the N=1 line.
+* ``5``: N = 262144, density 1e-3, fp64, ALG2, STRONG scaling over the ranks (north_star's
+  8-GPU configuration): rank r owns the rows [r0, r1) cut on the product-count prefix, B
+  (826 MB) broadcast inside every step.  At N > 1 it is also reported as the ``config5`` key
+  of the line (``--config5-n 0`` skips it).
+
+``python3 bench.py --gpus N`` (N > 1) without a launcher spawns N worker processes itself
+(before anything touches the GPU) with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, exactly
+as ``torch.distributed.run`` would; under a launcher (WORLD_SIZE set) it is one rank.
 
 Also reported: ``roofline`` for the numeric-phase kernel (compulsory bytes of the product,
 SURVEY 8d, / the phase's device time from HIP events on the library's stream, per launch),
 ``cpu_baseline`` = scipy's ``A @ B`` -- the reference's CPU comparator
 (SpGEMM_vs_SpMV/profiler.py:408) -- timed in forked children with their RSS growth, on
-rank 0 at N=1 (the whole product for config 2, a bounded row sample beyond), with the
-oracle's single-thread and OpenMP restatements beside it.
+rank 0 at N=1 (a bounded row sample of config 4), with the oracle's single-thread and OpenMP
+restatements beside it.
+
+``--device cpu --multiply-hook MOD:FN`` (tests only) runs the same multi-rank step logic on
+CPU tensors over gloo with the hook as the per-rank multiply (tests/test_bench_cpu.py).
 """
 from __future__ import annotations
 
 import argparse
+import importlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -45,13 +60,13 @@ CONFIGS = {
     "2": dict(n=16384, density=1e-3, alg=1, gen="scipy", steps=200, warmup=20,
               name="BASELINE config 2 (configs[1])"),
     "4": dict(n=65536, density=5e-3, alg=3, gen="device", steps=5, warmup=2,
-              name="BASELINE config 4 (ALG3 chunked, HBM-capped)"),
+              name="BASELINE config 4 (configs[3], ALG3 chunked, HBM-capped)"),
     "5": dict(n=262144, density=1e-3, alg=2, gen="device", steps=5, warmup=2,
-              name="BASELINE config 5 (row blocks, B broadcast)"),
+              name="BASELINE config 5 (configs[4], row blocks, B broadcast)"),
 }
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None, help="timed steps (default per config)")
@@ -65,9 +80,21 @@ def parse():
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="budget of the CPU-baseline sample (0 disables it)")
+    ap.add_argument("--no-config2", action="store_true", help="N=1: skip the config2 key")
+    ap.add_argument("--config5-n", type=int, default=262144,
+                    help="N>1: size of the strong-scaled config5 key (0 skips it)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="PMC traffic summary written by profiles/pmc_to_json.py")
-    return ap.parse_args()
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: tests only (gloo, --multiply-hook as the per-rank multiply)")
+    ap.add_argument("--multiply-hook", default=None,
+                    help="MOD:FN called as FN(A_block, B, wait_values) -> C (tests only)")
+    return ap.parse_args(argv)
+
+
+def pick(value, default):
+    """An explicit flag wins, including 0 (`args.alg or cfg` dropped --alg 0)."""
+    return default if value is None else value
 
 
 def compulsory_bytes(n_rows, n_cols, nnzA, nnzB, nnzC, vb, ib_c=4):
@@ -75,6 +102,50 @@ def compulsory_bytes(n_rows, n_cols, nnzA, nnzB, nnzC, vb, ib_c=4):
     (its row pointer ib_c bytes per entry: 8 once nnz(C) >= 2^31)."""
     return 4 * (n_rows + 1) + 4 * (n_cols + 1) + ib_c * (n_rows + 1) + (4 + vb) * (nnzA + nnzB + nnzC)
 
+
+# ------------------------------------------------------------------ launcher (no torchrun)
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_workers(n, argv):
+    """`--gpus N` without a launcher: start N fresh worker processes of this script (rank r
+    on GPU r), wait for all of them and return the worst exit status.  Runs before anything
+    touches the GPU and never re-execs this process.  Rank 0 prints the JSON line."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rcs = [None] * n
+    while any(rc is None for rc in rcs):
+        for i, p in enumerate(procs):
+            if rcs[i] is None:
+                rcs[i] = p.poll()
+        if any(rc not in (None, 0) for rc in rcs):   # one rank failed: end the others
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    p.terminate()
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    try:
+                        rcs[i] = p.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        rcs[i] = p.wait()
+            break
+        time.sleep(0.05)
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+# ------------------------------------------------------------------ measurement pieces
 
 def cpu_baseline(A_h, B_h, rows_sample, budget_s):
     """scipy A @ B (the reference's comparator) in forked children: median time and RSS
@@ -134,207 +205,363 @@ def traffic_for(pmc_path, key, build_id, source_id=None):
     return e.get("hbm_bytes_per_launch"), e.get("build_id")
 
 
-def main():
-    args = parse()
-    import torch
-    import torch.distributed as dist
+class Ctx:
+    """Device, rank and the collectives of one bench process."""
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    # one process per GPU; a rehearsal with more ranks than GPUs (SPG_DIST_BACKEND=gloo on a
-    # one-GPU box) puts several ranks on one device
-    local_dev = local % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local_dev)
-    dev = torch.device("cuda", local_dev)
-    if world > 1:
-        backend = os.environ.get("SPG_DIST_BACKEND", "nccl")   # nccl = RCCL on ROCm
-        dist.init_process_group(backend, **({"device_id": dev} if backend == "nccl" else {}))
+    def __init__(self, args):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        if self.world != args.gpus:
+            raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={self.world}")
+        self.gpu = args.device == "cuda"
+        if self.gpu:
+            # one process per GPU; a rehearsal with more ranks than GPUs (SPG_DIST_BACKEND=gloo
+            # on a one-GPU box) puts several ranks on one device
+            self.local_dev = local % max(1, torch.cuda.device_count())
+            torch.cuda.set_device(self.local_dev)
+            self.dev = torch.device("cuda", self.local_dev)
+        else:
+            self.local_dev, self.dev = None, torch.device("cpu")
+        if self.world > 1:
+            backend = os.environ.get("SPG_DIST_BACKEND", "nccl" if self.gpu else "gloo")   # nccl = RCCL
+            dist.init_process_group(backend, **({"device_id": self.dev} if backend == "nccl" else {}))
 
-    from spmm_amd import _lib, cusparse, distributed, gen
-    from spmm_amd.sparse import csr_matrix
+    def sync(self):
+        if self.gpu:
+            self.torch.cuda.synchronize()
 
-    cfg_name = args.config if args.config != "auto" else ("2" if world == 1 else "5")
-    cfg = dict(CONFIGS[cfg_name])
-    n = args.n or cfg["n"]
-    dens = args.density or cfg["density"]
-    alg = args.alg or cfg["alg"]
-    steps = args.steps if args.steps is not None else cfg["steps"]
-    warmup = args.warmup if args.warmup is not None else cfg["warmup"]
-    cf = args.chunk_fraction
-    if world > 1 and cfg_name != "5":
-        raise SystemExit("several GPUs run the row-block workload (config 5)")
-    npdt = np.float64 if args.dtype == "float64" else np.float32
-    tdt = torch.float64 if args.dtype == "float64" else torch.float32
-    vb = 8 if npdt == np.float64 else 4
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
 
-    # ---- inputs in HBM (not timed)
-    A_h = B_h = None
-    if cfg["gen"] == "scipy":
-        A_h, B_h = gen.scipy_pair(n, dens, seed=args.seed, dtype=npdt)
-        A, B = csr_matrix(A_h, device=dev), csr_matrix(B_h, device=dev)
-    else:
-        A = gen.random_csr(n, n, dens, seed=args.seed, dtype=tdt, device=dev)
-        B = gen.random_csr(n, n, dens, seed=args.seed + 1, dtype=tdt, device=dev) if rank == 0 or world == 1 else None
+    def reduce(self, vals, op):
+        """vals (floats) reduced over the ranks with `op` ("max" / "sum")."""
+        if self.world == 1:
+            return list(vals)
+        t = self.torch.tensor(list(vals), dtype=self.torch.float64, device=self.dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX if op == "max" else self.dist.ReduceOp.SUM)
+        return [float(x) for x in t.tolist()]
 
-    bcast_ms = None
-    rows = (0, n)
-    if world > 1:
-        # the row cut needs B's row lengths: one broadcast ahead of the timed steps (it also
-        # warms RCCL up), then this rank's block of A
-        Bw = distributed.broadcast_csr(B, 0, dev)
-        nnzB = Bw.nnz
-        rows, A, P_r = distributed.rowblock_setup(A, Bw.indptr, world, rank)
-        del Bw
-        torch.cuda.empty_cache()
-        ts = []
-        for _ in range(3):   # the broadcast alone (reported beside the step)
-            torch.cuda.synchronize(); dist.barrier()
-            t0 = time.perf_counter()
-            Bt = distributed.broadcast_csr(B, 0, dev)
-            torch.cuda.synchronize(); dist.barrier()
-            ts.append(time.perf_counter() - t0)
-            del Bt
-        bcast_ms = float(np.median(ts)) * 1e3
 
-        def step():
-            C, _ = distributed.rowblock_step(A, B, 0, dev, alg=alg, chunk_fraction=cf)
-            return C
-        P = P_r
-    else:
-        def step():
-            return cusparse.spgemm(A, B, alg=alg, chunk_fraction=cf)
-        P = cusparse.num_products(A, B)
-        nnzB = B.nnz
-
-    # ---- warmup, then exactly K timed steps between barrier + synchronize
-    C = None
+def timed(ctx, step, steps, warmup):
+    """W untimed steps, then exactly K timed steps between barrier + synchronize on both
+    sides.  Returns (seconds, the last step's result)."""
     for _ in range(warmup):
         C = step()
         del C
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    ctx.sync()
+    ctx.barrier()
     t0 = time.perf_counter()
+    C = None
     for i in range(steps):
         C = step()
         if i < steps - 1:
             del C
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    nnzC = C.nnz
-    ib_c = C.indptr.element_size()
-    peak_bytes = cusparse.last_stats.peak_bytes
-    del C
-    torch.cuda.empty_cache()
+    ctx.sync()
+    ctx.barrier()
+    return time.perf_counter() - t0, C
 
-    tot = torch.tensor([elapsed, float(P), float(nnzC), float(peak_bytes)], dtype=torch.float64, device=dev)
-    if world > 1:
-        mx = tot[:1].clone(); dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        sm = tot[1:3].clone(); dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        pk = tot[3:].clone(); dist.all_reduce(pk, op=dist.ReduceOp.MAX)
-        elapsed, P_all, nnz_all, peak_max = float(mx[0]), float(sm[0]), float(sm[1]), float(pk[0])
-    else:
-        P_all, nnz_all, peak_max = float(P), float(nnzC), float(peak_bytes)
-    ms_per_step = elapsed / steps * 1e3
-    gflops = 2.0 * P_all * steps / elapsed / 1e9
 
-    # ---- the other algorithms on the same inputs (config 2; after the timed region)
-    other = {}
-    if world == 1 and cfg_name == "2":
-        for a2 in (1, 2, 3):
-            if a2 == alg:
-                continue
-            for _ in range(3):
-                cusparse.spgemm(A, B, alg=a2, chunk_fraction=cf)
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            reps_o = max(5, steps // 2)
-            for _ in range(reps_o):
-                cusparse.spgemm(A, B, alg=a2, chunk_fraction=cf)
-            torch.cuda.synchronize()
-            dt = (time.perf_counter() - t0) / reps_o
-            other[f"alg{a2}"] = {"gflops": round(2.0 * P / dt / 1e9, 3), "ms_per_step": round(dt * 1e3, 5),
-                                 "peak_hbm_bytes": int(cusparse.last_stats.peak_bytes)}
-
-    # ---- per-phase device times (separate, instrumented pass after the timed region): HIP
-    # events on the library's stream, which is torch's current stream
-    h = _lib.get_handle(local_dev)
-    h.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+def phase_times(ctx, step, reps):
+    """Per-phase device times of `reps` extra steps (HIP events on the library's stream,
+    which is torch's current stream).  {} on CPU."""
+    if not ctx.gpu:
+        for _ in range(reps):
+            C = step()
+            del C
+        return {}
+    from spmm_amd import _lib
+    h = _lib.get_handle(ctx.local_dev)
+    h.set_stream(ctx.torch.cuda.current_stream(ctx.dev).cuda_stream)
     h.set_timing(True)
-    reps = 10 if cfg_name == "2" else 2
     for _ in range(reps):
         C = step()
         del C
-    phases = h.get_timing()
+    ph = h.get_timing()
     h.set_timing(False)
-    tile = cfg_name != "2"
-    num_kernel = "k_tile" if tile else "k_row"
-    num_ms, num_launches = phases["numeric"]
-    launches_per_product = max(1, num_launches // reps)
-    avg_num_ms = num_ms / max(num_launches, 1)
-    # this rank's product (its slab at N>1): algorithmic bytes, split over the numeric launches
-    bytes_product = compulsory_bytes(A.shape[0], n, A.nnz, nnzB, nnzC, vb, ib_c)
-    bytes_launch = bytes_product / launches_per_product
-    achieved = bytes_launch / (avg_num_ms * 1e-3) / 1e9
-    key = f"c{cfg_name}_n{n}_d{dens:g}_{args.dtype}_alg{alg}_w{world}"
-    traffic, traffic_build = traffic_for(args.pmc, key, _lib.build_id(), _lib.source_id())
+    return ph
 
-    # ---- CPU baseline (rank 0 at N=1): scipy A@B, the reference's comparator
+
+def roofline(phases, reps, kernel, bytes_product, ms_per_step, traffic, traffic_build, step_frac=True):
+    """`roofline` object of the numeric-phase kernel: algorithmic (compulsory) bytes of the
+    product split over its numeric launches / the average launch time from HIP events."""
+    num_ms, num_launches = phases.get("numeric", (0.0, 0))
+    if not num_launches:
+        return None
+    per = max(1, num_launches // reps)
+    avg = num_ms / num_launches
+    b_launch = bytes_product / per
+    achieved = b_launch / (avg * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_build_id": traffic_build,
+            "kernel": kernel + " (numeric phase)", "bytes_per_launch": int(b_launch),
+            "launches_per_product": per, "avg_launch_ms": round(avg, 5),
+            "step_frac": round(bytes_product / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if step_frac else None}
+
+
+def lib_ids(ctx):
+    if not ctx.gpu:
+        return None, None
+    from spmm_amd import _lib
+    return _lib.build_id(), _lib.source_id()
+
+
+def load_hook(spec):
+    if not spec:
+        return None
+    mod, fn = spec.split(":")
+    return getattr(importlib.import_module(mod), fn)
+
+
+def gen_device(ctx, n, dens, seed, tdt, rows=None, row_offset=0):
+    from spmm_amd import gen
+    return gen.random_csr(n if rows is None else rows, n, dens, seed=seed, dtype=tdt, device=ctx.dev,
+                          row_offset=row_offset)
+
+
+# ------------------------------------------------------------------ workloads
+
+def run_config4(ctx, args, cfg, tdt, vb, hook):
+    """Config 4 at N=1, weak-scaled row blocks at N > 1.  Returns the JSON line's fields."""
+    from spmm_amd import cusparse, distributed
+    n = pick(args.n, cfg["n"])
+    dens = pick(args.density, cfg["density"])
+    alg = pick(args.alg, cfg["alg"])
+    steps, warmup, cf = pick(args.steps, cfg["steps"]), pick(args.warmup, cfg["warmup"]), args.chunk_fraction
+    w, r = ctx.world, ctx.rank
+    # rank r's block of the (w*n) x n global A: rows [r*n, (r+1)*n); rank 0's is the N=1 A
+    A = gen_device(ctx, n, dens, args.seed, tdt, rows=n, row_offset=r * n)
+    B = gen_device(ctx, n, dens, args.seed + 1, tdt) if (r == 0 or w == 1) else None
+    bcast_ms = None
+    if w > 1:
+        Bw = distributed.broadcast_csr(B, 0, ctx.dev)   # warms RCCL up; B's row lengths
+        P = int(distributed.product_prefix(A, Bw.indptr)[-1])
+        nnzB = Bw.nnz
+        del Bw
+        bcast_ms = broadcast_ms(ctx, B)
+
+        def step():
+            C, _ = distributed.rowblock_step(A, B, 0, ctx.dev, alg=alg, chunk_fraction=cf, multiply=hook)
+            return C
+    else:
+        P, nnzB = cusparse.num_products(A, B), B.nnz
+
+        def step():
+            return cusparse.spgemm(A, B, alg=alg, chunk_fraction=cf)
+    elapsed, C = timed(ctx, step, steps, warmup)
+    nnzC, ib_c = C.nnz, C.indptr.element_size()
+    peak = last_peak(ctx)
+    del C
+    if ctx.gpu:
+        ctx.torch.cuda.empty_cache()
+    (elapsed,) = ctx.reduce([elapsed], "max")
+    P_all, nnz_all = ctx.reduce([float(P), float(nnzC)], "sum")
+    (peak_max,) = ctx.reduce([float(peak)], "max")
+    ms = elapsed / steps * 1e3
+    reps = 2
+    ph = phase_times(ctx, step, reps)
+    bid, sid = lib_ids(ctx)
+    key = f"c4_n{n}_d{dens:g}_{args.dtype}_alg{alg}_w1"   # per-rank work = the N=1 product
+    traffic, tb = traffic_for(args.pmc, key, bid, sid) if ctx.gpu else (None, None)
+    rf = roofline(ph, reps, "k_tile", compulsory_bytes(A.shape[0], n, A.nnz, nnzB, nnzC, vb, ib_c),
+                  ms, traffic, tb, step_frac=(w == 1))
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        if A_h is None:   # configs 4/5: a bounded row sample of the same A, all of B
-            A_h, B_h = A.get(), B.get()
-            sample = np.sort(np.random.default_rng(0).choice(n, size=min(n, 1024), replace=False))
-        else:
-            sample = None
+    if r == 0 and w == 1 and args.cpu_seconds > 0 and ctx.gpu:
+        A_h, B_h = A.get(), B.get()
+        sample = np.sort(np.random.default_rng(0).choice(n, size=min(n, 1024), replace=False))
         cpu = cpu_baseline(A_h, B_h, sample, args.cpu_seconds)
+    desc = (f"{cfg['name']}: random CSR {n}x{n} density={dens:g} {args.dtype} "
+            f"(spmm_amd.gen.random_csr on the device, seeds {args.seed}/{args.seed + 1}), "
+            f"ALG{alg} chunked, chunk_fraction {cf}")
+    if w > 1:
+        desc += (f"; weak scaling: rank r owns rows [r*{n}, (r+1)*{n}) of a {w * n}x{n} A "
+                 "(rank 0's block is the N=1 A), B broadcast over RCCL inside every step, no reduction")
+    out = {
+        "value": round(2.0 * P_all * steps / elapsed / 1e9, 3), "steps": steps, "warmup": warmup,
+        "ms_per_step": round(ms, 5), "scaling": "weak",
+        "config": {"workload": desc, "N": n, "rows_per_rank": n, "density": dens, "alg": alg,
+                   "chunk_fraction": cf, "nnzB": int(nnzB), "nnzA_rank0" if w > 1 else "nnzA": int(A.nnz),
+                   "nnzC": int(nnz_all), "num_products": int(P_all),
+                   "parallelism": "single GPU" if w == 1 else f"row-block x{w} (weak), B broadcast over RCCL"},
+        "peak_hbm_bytes": int(peak_max), "roofline": rf,
+        "phases_ms_per_step": {k: round(v[0] / reps, 5) for k, v in ph.items() if v[1]},
+        "b_broadcast_ms": None if bcast_ms is None else round(bcast_ms, 3),
+        "cpu_baseline": cpu,
+    }
+    del A, B
+    return out
 
-    if rank == 0:
-        step_desc = {"2": "ALG1 single-pass numeric", "4": f"ALG{alg} chunked, chunk_fraction {cf}",
-                     "5": f"ALG{alg}"}[cfg_name]
-        line = {
-            "metric": METRIC, "value": round(gflops, 3), "unit": "GFLOPS", "n_gpus": world,
-            "steps": steps, "warmup": warmup, "ms_per_step": round(ms_per_step, 5),
-            "higher_is_better": True, "scaling": "strong" if cfg_name == "5" else "weak",
-            "vs_baseline": None, "dtype": "f64" if vb == 8 else "f32", "data": "synthetic",
-            "config": {
-                "workload": (f"{cfg['name']}: random CSR {n}x{n} density={dens:g} {args.dtype} "
-                             + ("(scipy.sparse.random, default_rng(42); A then B), " if cfg["gen"] == "scipy"
-                                else f"(spmm_amd.gen.random_csr on the device, seeds {args.seed}/{args.seed + 1}), ")
-                             + step_desc
-                             + ("" if world == 1 else
-                                f"; {world} row blocks cut on the product prefix, B broadcast over RCCL inside every step")),
-                "N": n, "density": dens, "alg": alg, "nnzB": int(nnzB),
-                ("nnzA" if world == 1 else "nnzA_rank0"): int(A.nnz),
-                "nnzC": int(nnz_all), "num_products": int(P_all),
-                "parallelism": "single GPU" if world == 1 else f"row-block x{world}, B broadcast over RCCL",
-            },
-            "peak_hbm_bytes": int(peak_max),
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "traffic_build_id": traffic_build,
-                         "kernel": num_kernel + " (numeric phase)",
-                         "bytes_per_launch": int(bytes_launch), "launches_per_product": launches_per_product,
-                         "avg_launch_ms": round(avg_num_ms, 5),
-                         "step_frac": round(bytes_product / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-                         if world == 1 else None},
-            "phases_ms_per_step": {k: round(v[0] / reps, 5) for k, v in phases.items() if v[1]},
-            "b_broadcast_ms": None if bcast_ms is None else round(bcast_ms, 3),
-            "rows_rank0": list(rows),
-            "cpu_baseline": cpu,
-            "other_algs": other or None,
-            "lib_build_id": _lib.build_id(),
-        }
+
+def broadcast_ms(ctx, B):
+    """The B broadcast alone (median of 3), reported beside the step."""
+    from spmm_amd import distributed
+    ts = []
+    for _ in range(3):
+        ctx.sync()
+        ctx.barrier()
+        t0 = time.perf_counter()
+        Bt = distributed.broadcast_csr(B, 0, ctx.dev)
+        ctx.sync()
+        ctx.barrier()
+        ts.append(time.perf_counter() - t0)
+        del Bt
+    return float(np.median(ts)) * 1e3
+
+
+def last_peak(ctx):
+    if not ctx.gpu:
+        return 0
+    from spmm_amd import cusparse
+    return cusparse.last_stats.peak_bytes
+
+
+def run_config5(ctx, args, cfg, n, tdt, vb, hook, steps, warmup):
+    """Config 5 strong-scaled: the rows of one n x n A cut on the product prefix over the
+    ranks (each rank draws only its own block), B broadcast inside every step."""
+    from spmm_amd import cusparse, distributed
+    dens, alg, cf = cfg["density"], cfg["alg"], args.chunk_fraction
+    w, r = ctx.world, ctx.rank
+    B = gen_device(ctx, n, dens, args.seed + 1, tdt) if (r == 0 or w == 1) else None
+    if w > 1:
+        Bw = distributed.broadcast_csr(B, 0, ctx.dev)
+        nnzB = Bw.nnz
+
+        def draw(rows, off):
+            return gen_device(ctx, n, dens, args.seed, tdt, rows=rows, row_offset=off)
+        rows, A, P = distributed.rowblock_setup_drawn(draw, n, Bw.indptr, w, r)
+        del Bw
+        if ctx.gpu:
+            ctx.torch.cuda.empty_cache()
+        bcast_ms = broadcast_ms(ctx, B)
+
+        def step():
+            C, _ = distributed.rowblock_step(A, B, 0, ctx.dev, alg=alg, chunk_fraction=cf, multiply=hook)
+            return C
+    else:
+        A = gen_device(ctx, n, dens, args.seed, tdt)
+        rows, P, nnzB, bcast_ms = (0, n), cusparse.num_products(A, B), B.nnz, None
+
+        def step():
+            return cusparse.spgemm(A, B, alg=alg, chunk_fraction=cf)
+    elapsed, C = timed(ctx, step, steps, warmup)
+    nnzC, ib_c = C.nnz, C.indptr.element_size()
+    peak = last_peak(ctx)
+    del C
+    if ctx.gpu:
+        ctx.torch.cuda.empty_cache()
+    (elapsed,) = ctx.reduce([elapsed], "max")
+    P_all, nnz_all = ctx.reduce([float(P), float(nnzC)], "sum")
+    (peak_max,) = ctx.reduce([float(peak)], "max")
+    ms = elapsed / steps * 1e3
+    reps = 1
+    ph = phase_times(ctx, step, reps)
+    rf = roofline(ph, reps, "k_tile", compulsory_bytes(A.shape[0], n, A.nnz, nnzB, nnzC, vb, ib_c),
+                  ms, None, None, step_frac=False)
+    out = {"gflops": round(2.0 * P_all * steps / elapsed / 1e9, 3), "ms_per_step": round(ms, 5),
+           "steps": steps, "warmup": warmup, "scaling": "strong", "N": n, "density": dens, "alg": alg,
+           "num_products": int(P_all), "nnzC": int(nnz_all), "rows_rank0": list(rows),
+           "peak_hbm_bytes_max_rank": int(peak_max), "b_broadcast_ms": None if bcast_ms is None else round(bcast_ms, 3),
+           "roofline_rank0": rf,
+           "workload": (f"{cfg['name']}: random CSR {n}x{n} density={dens:g} {args.dtype}, ALG{alg}; "
+                        f"{w} row blocks cut on the product prefix (each rank draws its own block), "
+                        "B broadcast over RCCL inside every step")}
+    del A, B
+    return out
+
+
+def run_config2(ctx, args, cfg, npdt, vb, with_cpu):
+    """Config 2 (ALG1, N=16384) on one GPU: GFLOPS, its k_row roofline and the other ALGs."""
+    from spmm_amd import _lib, cusparse, gen
+    from spmm_amd.sparse import csr_matrix
+    n, dens, alg, cf = cfg["n"], cfg["density"], cfg["alg"], args.chunk_fraction
+    A_h, B_h = gen.scipy_pair(n, dens, seed=args.seed, dtype=npdt)
+    A, B = csr_matrix(A_h, device=ctx.dev), csr_matrix(B_h, device=ctx.dev)
+    P = cusparse.num_products(A, B)
+    steps, warmup = cfg["steps"], cfg["warmup"]
+
+    def step():
+        return cusparse.spgemm(A, B, alg=alg, chunk_fraction=cf)
+    elapsed, C = timed(ctx, step, steps, warmup)
+    nnzC, ib_c = C.nnz, C.indptr.element_size()
+    peak = cusparse.last_stats.peak_bytes
+    del C
+    ms = elapsed / steps * 1e3
+    other = {}
+    for a2 in (2, 3):
+        t, _ = timed(ctx, lambda: cusparse.spgemm(A, B, alg=a2, chunk_fraction=cf), max(5, steps // 2), 3)
+        dt = t / max(5, steps // 2)
+        other[f"alg{a2}"] = {"gflops": round(2.0 * P / dt / 1e9, 3), "ms_per_step": round(dt * 1e3, 5),
+                             "peak_hbm_bytes": int(cusparse.last_stats.peak_bytes)}
+    reps = 10
+    ph = phase_times(ctx, step, reps)
+    key = f"c2_n{n}_d{dens:g}_{args.dtype}_alg{alg}_w1"
+    traffic, tb = traffic_for(args.pmc, key, _lib.build_id(), _lib.source_id())
+    rf = roofline(ph, reps, "k_row", compulsory_bytes(n, n, A.nnz, B.nnz, nnzC, vb, ib_c), ms, traffic, tb)
+    out = {"gflops": round(2.0 * P * steps / elapsed / 1e9, 3), "ms_per_step": round(ms, 5),
+           "steps": steps, "warmup": warmup, "N": n, "density": dens, "alg": alg, "nnzC": int(nnzC),
+           "num_products": int(P), "peak_hbm_bytes": int(peak), "roofline": rf,
+           "phases_ms_per_step": {k: round(v[0] / reps, 5) for k, v in ph.items() if v[1]},
+           "other_algs": other,
+           "workload": (f"{cfg['name']}: random CSR {n}x{n} density={dens:g} {args.dtype} "
+                        "(scipy.sparse.random, default_rng(42); A then B), ALG1 single-pass numeric")}
+    if with_cpu and args.cpu_seconds > 0:
+        out["cpu_baseline"] = cpu_baseline(A_h, B_h, None, args.cpu_seconds)
+    return out
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_workers(args.gpus, argv)   # before any GPU call; no re-exec
+    ctx = Ctx(args)
+    hook = load_hook(args.multiply_hook)
+    if hook is None and not ctx.gpu:
+        raise SystemExit("--device cpu needs --multiply-hook (the product path runs on the GPU only)")
+    torch = ctx.torch
+    npdt = np.float64 if args.dtype == "float64" else np.float32
+    tdt = torch.float64 if args.dtype == "float64" else torch.float32
+    vb = 8 if npdt == np.float64 else 4
+    name = args.config if args.config != "auto" else "4"
+    if ctx.world > 1 and name == "2":
+        raise SystemExit("several GPUs run the row-block workloads (config 4 weak, config 5 strong)")
+
+    line = {"metric": METRIC, "unit": "GFLOPS", "n_gpus": ctx.world, "higher_is_better": True,
+            "vs_baseline": None, "dtype": "f64" if vb == 8 else "f32", "data": "synthetic"}
+    if name == "4":
+        res = run_config4(ctx, args, CONFIGS["4"], tdt, vb, hook)
+        line.update(res)
+        if ctx.world == 1 and ctx.gpu and not args.no_config2:
+            line["config2"] = run_config2(ctx, args, CONFIGS["2"], npdt, vb, with_cpu=False)
+        if ctx.world > 1 and args.config5_n > 0:
+            line["config5"] = run_config5(ctx, args, CONFIGS["5"], args.config5_n, tdt, vb, hook,
+                                          steps=3, warmup=1)
+    elif name == "5":
+        cfg = CONFIGS["5"]
+        res = run_config5(ctx, args, cfg, pick(args.n, cfg["n"]), tdt, vb, hook,
+                          pick(args.steps, cfg["steps"]), pick(args.warmup, cfg["warmup"]))
+        line.update({"value": res.pop("gflops"), "steps": res.pop("steps"), "warmup": res.pop("warmup"),
+                     "ms_per_step": res.pop("ms_per_step"), "scaling": res.pop("scaling"),
+                     "config": res, "peak_hbm_bytes": res.pop("peak_hbm_bytes_max_rank"),
+                     "roofline": res.pop("roofline_rank0")})
+    else:   # config 2 as the line (one GPU)
+        res = run_config2(ctx, args, CONFIGS["2"], npdt, vb, with_cpu=ctx.rank == 0)
+        line.update({"value": res.pop("gflops"), "steps": res.pop("steps"), "warmup": res.pop("warmup"),
+                     "ms_per_step": res.pop("ms_per_step"), "scaling": "weak",
+                     "peak_hbm_bytes": res.pop("peak_hbm_bytes"), "roofline": res.pop("roofline"),
+                     "cpu_baseline": res.pop("cpu_baseline", None), "config": res})
+    line["lib_build_id"] = lib_ids(ctx)[0]
+    if ctx.rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    if ctx.world > 1:
+        ctx.barrier()
+        ctx.dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -27,10 +27,13 @@
  *     host; the caller then allocates C's indices/values and calls spg_numeric (like
  *     cusparseSpMatGetSize -> cusparseCsrSetPointers -> cusparseSpGEMM_copy).
  *   - Stream ordering: every call enqueues on the handle's stream.  The only calls that
- *     wait on the device are spg_plan for ALG1/ALG3 (to size buffers from the product
- *     count), spg_num_products, spg_symbolic (nnz(C) to host) and spg_validate_csr.
- *     spg_symbolic waits only for nnz(C): under ALG1 it returns while the numeric pass it
- *     queued is still running, so C is ready in stream order, not on return.
+ *     wait on the device are spg_plan for ALG3 (its chunk plan reads the product-count
+ *     prefix back) and for ALG1 on shapes outside the short-row kernel (the upper-bound
+ *     buffer is sized from the product count), spg_num_products, spg_symbolic (nnz(C) to
+ *     host) and spg_validate_csr.  spg_plan for ALG1 on short-row shapes does no device work
+ *     (its output buffer is sized from the expected product count).  spg_symbolic waits
+ *     only for nnz(C): under ALG1 it returns while the numeric pass it queued is still
+ *     running, so C is ready in stream order, not on return.
  *   - Errors are status codes only; the library never calls exit().  SPG_STATUS_ALLOC_FAILED
  *     lets a harness print "[SKIP]" (dense_vs_sparseGEMM/utils.py:156-173).
  *   - A handle is not thread-safe: one handle per host thread per device (mirrors CuPy's
@@ -83,8 +86,13 @@ typedef enum { SPG_R_32F = 0, SPG_R_64F = 1, SPG_C_32F = 4, SPG_C_64F = 5 } spg_
 /* Algorithm selector (cusparseSpGEMMAlg_t roles, cupy-src/cupy_backends/cuda/libs/
  * cusparse.pxd:158-164; chosen at cupy-src/cupyx/cusparse.py:2052-2057):
  *   SPG_ALG_DEFAULT  library choice (currently ALG2);
- *   SPG_ALG1  single pass: one kernel computes structure and values into an upper-bound
- *             buffer (workspace ~ num_products), spg_numeric compacts it into C -- the
+ *   SPG_ALG1  one numeric pass, one host sync: on short-row shapes a count pass (nnz per
+ *             row) and ONE numeric launch that also scans the counts into C's row pointer
+ *             and writes C compact into an estimate-sized workspace buffer (an output past
+ *             the estimate is redone two-phase into C); spg_numeric then copies/scales it
+ *             (or only scales, when C's arrays are that buffer: spg_result_in_workspace).
+ *             Other shapes: a single pass into an upper-bound buffer (workspace ~
+ *             num_products) that spg_numeric compacts, or (tile path) two phases -- the
  *             memory-hungry / fewest-passes point, like cuSPARSE ALG1;
  *   SPG_ALG2  two phase: symbolic (nnz per row) then numeric straight into C; workspace is
  *             O(rows + nnz(A));
@@ -113,6 +121,11 @@ typedef struct spg_plan_s *spg_plan_t;
 
 /* Library version as MAJOR*10000 + MINOR*100 + PATCH (cusparseGetVersion). */
 int spg_version(void);
+
+/* Build stamp of the loaded library: "source_id=<16 hex> hipflags=<flags>", the id being a
+ * hash of the sources and the compile flags it was built from (spmm_amd/source_id.py).
+ * Measurements are stamped with it.  No cuSPARSE counterpart. */
+const char *spg_build_info(void);
 
 /* Human-readable status name (cusparseGetErrorString). */
 const char *spg_status_string(spg_status_t status);

@@ -40,7 +40,7 @@ STATUS_ALLOC_FAILED = 2
 STATUS_OVERFLOW = 100
 
 # every symbol include/spgemm.h declares (tests/test_abi.py checks the .so exports them)
-EXPORTS = ("spg_version", "spg_status_string", "spg_create", "spg_destroy", "spg_set_stream",
+EXPORTS = ("spg_version", "spg_build_info", "spg_status_string", "spg_create", "spg_destroy", "spg_set_stream",
            "spg_last_hip_error", "spg_plan", "spg_num_products", "spg_symbolic",
            "spg_numeric", "spg_peak_bytes", "spg_validate_csr", "spg_plan_destroy",
            "spg_set_timing", "spg_get_timing", "spg_result_in_workspace", "spg_spmv",
@@ -93,6 +93,7 @@ def load():
         csrp = ctypes.POINTER(SpgCsr)
         proto = {
             "spg_version": (ctypes.c_int, []),
+            "spg_build_info": (ctypes.c_char_p, []),
             "spg_status_string": (ctypes.c_char_p, [ctypes.c_int]),
             "spg_create": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.c_int]),
             "spg_destroy": (ctypes.c_int, [vp]),
@@ -140,27 +141,16 @@ _source_id = None
 
 
 def source_id() -> str:
-    """First 16 hex digits of the SHA-256 of the sources the library is compiled from
-    (spmm_amd/csrc/*.hip, *.hpp, include/*.h, the Makefile's flags).  hipcc's output is not
-    byte-identical from one build to the next, so a rebuild of the same sources changes
-    build_id() but not this; measurements carry both."""
+    """The source id compiled INTO the loaded library (spg_build_info; spmm_amd/source_id.py:
+    a hash of the sources and the effective HIPFLAGS it was built from).  hipcc's output is
+    not byte-identical from one build to the next, so a rebuild of the same sources changes
+    build_id() but not this; an A/B build (SPG_LIB), a stale .so or a HIPFLAGS variant
+    reports its own id.  Measurements carry both."""
     global _source_id
     if _source_id is None:
-        import glob
-        import hashlib
-        root = os.path.dirname(_HERE)
-        files = sorted(glob.glob(os.path.join(_HERE, "csrc", "*.hip")) + glob.glob(os.path.join(_HERE, "csrc", "*.hpp"))
-                       + glob.glob(os.path.join(root, "include", "*.h")))
-        h = hashlib.sha256()
-        for fn in files:
-            h.update(os.path.basename(fn).encode())
-            with open(fn, "rb") as f:
-                h.update(f.read())
-        mk = os.path.join(root, "Makefile")
-        if os.path.exists(mk):
-            with open(mk) as f:
-                h.update("".join(l for l in f if l.startswith(("HIPFLAGS", "ARCH"))).encode())
-        _source_id = h.hexdigest()[:16]
+        info = (load().spg_build_info() or b"").decode()
+        sid = dict(kv.split("=", 1) for kv in info.split() if "=" in kv).get("source_id", "unknown")
+        _source_id = sid
     return _source_id
 
 

@@ -143,19 +143,25 @@ inline bool row_kernel_enabled() {
     return on;
 }
 
-// Tile numeric kernel variant (A/B timing): SPG_TILE_RU = chunks per owner-round group
-// (1, 2, or all in flight), SPG_TILE_DENSE=0 turns the column-addressed accumulator off.
-struct TileVariant { int ru; bool dense; int diag; };
+// Tile numeric kernel variant (A/B timing builds only: `make HIPFLAGS+=-DSPG_TILE_RU=2` etc.;
+// no environment variable can change what the shipped library computes).
+//   SPG_TILE_RU     chunks per owner-round group (1, 2, or all in flight)
+//   SPG_TILE_DENSE  0 turns the column-addressed accumulator off
+//   SPG_TILE_TWS    log2 of a forced tile width (8..12; 0 = the planner's choice)
+// The timing-only diagnostics (SPG_TILE_DIAG, results wrong) exist only in spgemm_tile.hpp
+// builds that define it.
+#ifndef SPG_TILE_RU
+#define SPG_TILE_RU 1
+#endif
+#ifndef SPG_TILE_DENSE
+#define SPG_TILE_DENSE 1
+#endif
+#ifndef SPG_TILE_TWS
+#define SPG_TILE_TWS 0
+#endif
+struct TileVariant { int ru; bool dense; };
 inline const TileVariant& tile_variant() {
-    static const TileVariant v = [] {
-        TileVariant t{1, true, 0};
-        if (const char* e = std::getenv("SPG_TILE_RU")) t.ru = std::atoi(e);
-        if (const char* e = std::getenv("SPG_TILE_DENSE")) t.dense = std::atoi(e) != 0;
-        // timing-only diagnostics (results wrong): 1 = no accumulation, 2 = no record loads,
-        // 4 = no product batches, 8 = no output stores (dense tiles)
-        if (const char* e = std::getenv("SPG_TILE_DIAG")) t.diag = std::atoi(e);
-        return t;
-    }();
+    static const TileVariant v{SPG_TILE_RU, SPG_TILE_DENSE != 0};
     return v;
 }
 
@@ -189,10 +195,7 @@ inline bool want_tile(const spg_csr_t& A, const spg_csr_t& B, int& tws, int& G) 
         if (tw <= TILE_CAP || frac * tw <= 0.95 * TILE_CAP) tws = t;
         if (tw >= (double)B.cols) break;
     }
-    if (const char* e = std::getenv("SPG_TILE_TWS")) {   // A/B timing: force the tile width
-        const int t = std::atoi(e);
-        if (t >= 8 && t <= 12) tws = t;
-    }
+    if (SPG_TILE_TWS >= 8 && SPG_TILE_TWS <= 12) tws = SPG_TILE_TWS;   // A/B timing builds only
     if (frac * (double)(1 << tws) < 64.0) return false;
     // the tile-major B's segment table is int32 and its records are addressed with 32-bit
     // byte offsets
@@ -869,7 +872,7 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
                                   h->stream, kt.a, kt.b, 0, r0, n, p.tws, p.G, Ap, Aj, Ax, p.B.rows,
                                   (const uint32_t*)p.brec, (const int32_t*)p.tptr,
                                   dense ? (const uint32_t*)nullptr : (const uint32_t*)p.bitmap,
-                                  (const int64_t*)tile_chunk_items(p, c), cj, cx, alpha, tile_variant().diag);
+                                  (const int64_t*)tile_chunk_items(p, c), cj, cx, alpha);
         };
         constexpr int UF = sizeof(T) > 8 ? 4 : 8;
         using D1 = std::integral_constant<bool, true>;
@@ -1053,6 +1056,14 @@ spg_status_t validate_typed(spg_handle_t h, const spg_csr_t& M, int* flags) {
 extern "C" {
 
 int spg_version(void) { return SPG_VERSION_MAJOR * 10000 + SPG_VERSION_MINOR * 100 + SPG_VERSION_PATCH; }
+
+#ifndef SPG_SOURCE_ID
+#define SPG_SOURCE_ID "unknown"
+#endif
+#ifndef SPG_HIPFLAGS
+#define SPG_HIPFLAGS ""
+#endif
+const char* spg_build_info(void) { return "source_id=" SPG_SOURCE_ID " hipflags=" SPG_HIPFLAGS; }
 
 const char* spg_status_string(spg_status_t s) {
     switch (s) {

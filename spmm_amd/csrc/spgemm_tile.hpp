@@ -373,13 +373,20 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile_sym(
 // (round, chunk, lane) per product, the product whose key stuck adds, the others retry with
 // the next (smaller) round number.  Within a group the lowest (chunk, lane) -- the earliest
 // product in flattened order -- of every position adds first; groups run in order.
+// Timing-only diagnostics of k_tile (results WRONG; A/B timing builds only, never shipped):
+// 1 = no accumulation, 2 = no record loads, 4 = no product batches, 8 = no output stores.
+#ifndef SPG_TILE_DIAG
+#define SPG_TILE_DIAG 0
+#endif
+
 template <typename T, typename IP, bool DENSE, int RU>
 __global__ __launch_bounds__(tile_num_wpb<DENSE>() * WAVE) void k_tile(
     int64_t row0, int64_t nrows, int tws, int G, const IP* __restrict__ Ap,
     const int32_t* __restrict__ Aj, const T* __restrict__ Ax, int64_t K,
     const uint32_t* __restrict__ brec, const int32_t* __restrict__ tptr,
     const uint32_t* __restrict__ bitmap, const int64_t* __restrict__ item_off,
-    int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha, int diag) {
+    int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha) {
+    constexpr int diag = SPG_TILE_DIAG;   // 0 in every shipped build (timing-only diagnostics)
     constexpr int U = sizeof(T) > 8 ? 4 : 8;   // chunks in flight (complex128: half)
     static_assert(U % RU == 0, "round groups split the chunks in flight");
     constexpr int WPB = tile_num_wpb<DENSE>();
@@ -590,10 +597,10 @@ __global__ __launch_bounds__(tile_num_wpb<DENSE>() * WAVE) void k_tile(
                                 while (__ballot(gm != 0u)) {
                                     const uint32_t kb = (seq << 9) | (uint32_t)l;
 #pragma unroll
-                                    for (int u = u0; u < u0 + RG; ++u)
+                                    for (int u = u0; u < u0 + RG && u < NU; ++u)
                                         if (gm & (1u << u)) atomicMin(&S.tag[pos[u]], kb | ((uint32_t)u << 6));
 #pragma unroll
-                                    for (int u = u0; u < u0 + RG; ++u)
+                                    for (int u = u0; u < u0 + RG && u < NU; ++u)
                                         if ((gm & (1u << u)) &&
                                             __hip_atomic_load(&S.tag[pos[u]], __ATOMIC_RELAXED,
                                                               __HIP_MEMORY_SCOPE_WAVEFRONT) == (kb | ((uint32_t)u << 6))) {

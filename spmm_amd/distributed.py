@@ -139,6 +139,29 @@ def rowblock_setup(A: csr_matrix, b_indptr: torch.Tensor, world: int, rank: int)
     return (r0, r1), row_slice(A, r0, r1), int(pref[r1] - pref[r0])
 
 
+def rowblock_setup_drawn(draw, n_rows: int, b_indptr: torch.Tensor, world: int, rank: int, group=None):
+    """rowblock_setup without any rank holding all of A: `draw(rows, row_offset)` returns
+    rows [row_offset, row_offset + rows) of the global A (spmm_amd.gen.random_csr draws any
+    row range of its matrix).  Every rank draws an equal-row block, its per-row product
+    counts are gathered, every rank cuts the global product prefix the same way, and a rank
+    whose cut block differs draws it.  Returns ((r0, r1), A_block, P_r)."""
+    q = [(n_rows * r) // world for r in range(world + 1)]
+    A0 = draw(q[rank + 1] - q[rank], q[rank])
+    pre = product_prefix(A0, b_indptr)
+    per_row = (pre[1:] - pre[:-1]).to(torch.int64)
+    width = max(q[r + 1] - q[r] for r in range(world))
+    mine = torch.zeros(width, dtype=torch.int64, device=per_row.device)
+    mine[:per_row.numel()] = per_row
+    parts = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(parts, mine, group=group)
+    counts = torch.cat([parts[r][:q[r + 1] - q[r]] for r in range(world)]).cpu().numpy()
+    pref = np.zeros(n_rows + 1, dtype=np.int64)
+    np.cumsum(counts, out=pref[1:])
+    r0, r1 = row_blocks(n_rows, world, pref)[rank]
+    A = A0 if (r0, r1) == (q[rank], q[rank + 1]) else draw(r1 - r0, r0)
+    return (r0, r1), A, int(pref[r1] - pref[r0])
+
+
 def rowblock_step(A_block: csr_matrix, B_src: csr_matrix | None, src: int, device, alg: int = 2,
                   chunk_fraction: float = 0.2, multiply=None, group=None):
     """One C = A.B step of the row-block scheme on this rank: B arrives from `src` (its
