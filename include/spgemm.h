@@ -207,6 +207,22 @@ spg_status_t spg_peak_bytes(spg_plan_t plan, size_t *bytes);
  * bounds or bad indptr.  Waits for the device. */
 spg_status_t spg_validate_csr(spg_handle_t handle, const spg_csr_t *M, int *is_canonical);
 
+/* What a plan will run (a diagnostic for tests and profilers; no cuSPARSE counterpart, the
+ * closest being the chunk plan cusparseSpGEMM_estimateMemory makes internally,
+ * spgemm_from_txt_alg3.cu:195-202).  path: 0 general windowed kernels, 1 short-row kernel,
+ * 2 tile path (tile_width columns per numeric tile, tiles_per_row tiles, dense_tiles 1
+ * when the accumulator is addressed by column).  n_chunks row chunks (ALG3: the chunk
+ * cut; otherwise 1); their n_chunks + 1 row boundaries go to chunk_rows (at most
+ * `capacity` entries written; chunk_rows may be NULL when capacity is 0). */
+typedef struct {
+    int path;
+    int tile_width;
+    int64_t tiles_per_row;
+    int dense_tiles;
+    int64_t n_chunks;
+} spg_plan_info_t;
+spg_status_t spg_plan_info(spg_plan_t plan, spg_plan_info_t *info, int64_t *chunk_rows, int64_t capacity);
+
 /* Free a plan's host metadata (cusparseSpGEMM_destroyDescr).  Never touches the
  * caller's workspace. */
 spg_status_t spg_plan_destroy(spg_plan_t plan);

@@ -44,7 +44,7 @@ EXPORTS = ("spg_version", "spg_build_info", "spg_status_string", "spg_create", "
            "spg_last_hip_error", "spg_plan", "spg_num_products", "spg_symbolic",
            "spg_numeric", "spg_peak_bytes", "spg_validate_csr", "spg_plan_destroy",
            "spg_set_timing", "spg_get_timing", "spg_result_in_workspace", "spg_spmv",
-           "spg_spgemm_ws")
+           "spg_spgemm_ws", "spg_plan_info")
 
 PHASES = ("products", "scan", "symbolic", "numeric", "compact", "validate", "spill", "spmv")
 NUM_PHASES = 8
@@ -56,6 +56,12 @@ class SpgCsr(ctypes.Structure):
                 ("indptr", ctypes.c_void_p), ("indices", ctypes.c_void_p),
                 ("values", ctypes.c_void_p), ("indptr_type", ctypes.c_int),
                 ("value_type", ctypes.c_int)]
+
+
+class SpgPlanInfo(ctypes.Structure):
+    """spg_plan_info_t"""
+    _fields_ = [("path", ctypes.c_int), ("tile_width", ctypes.c_int), ("tiles_per_row", ctypes.c_int64),
+                ("dense_tiles", ctypes.c_int), ("n_chunks", ctypes.c_int64)]
 
 
 class SpgTiming(ctypes.Structure):
@@ -109,6 +115,7 @@ def load():
             "spg_peak_bytes": (ctypes.c_int, [vp, ctypes.POINTER(sz)]),
             "spg_validate_csr": (ctypes.c_int, [vp, csrp, ctypes.POINTER(ctypes.c_int)]),
             "spg_plan_destroy": (ctypes.c_int, [vp]),
+            "spg_plan_info": (ctypes.c_int, [vp, ctypes.POINTER(SpgPlanInfo), ctypes.POINTER(i64), i64]),
             "spg_spgemm_ws": (ctypes.c_int, [vp, csrp, csrp, ctypes.c_int, ctypes.c_float, vp, vp, sz, vp,
                                              ctypes.c_int, ctypes.POINTER(i64), ctypes.POINTER(vp),
                                              ctypes.POINTER(vp), ctypes.POINTER(sz), ctypes.POINTER(vp)]),

@@ -1533,6 +1533,19 @@ spg_status_t spg_validate_csr(spg_handle_t h, const spg_csr_t* M, int* is_canoni
     return SPG_STATUS_SUCCESS;
 }
 
+spg_status_t spg_plan_info(spg_plan_t p, spg_plan_info_t* info, int64_t* chunk_rows, int64_t capacity) {
+    if (!p || !info || capacity < 0 || (capacity > 0 && !chunk_rows)) return SPG_STATUS_INVALID_VALUE;
+    info->path = p->use_tile ? 2 : (p->use_short ? 1 : 0);
+    info->tile_width = p->use_tile ? (1 << p->tws) : 0;
+    info->tiles_per_row = p->use_tile ? p->G : 0;
+    info->dense_tiles = tile_dense(*p) ? 1 : 0;
+    const bool chunked = p->alg == SPG_ALG3 && p->chunk_rows.size() > 1;
+    info->n_chunks = chunked ? (int64_t)p->chunk_rows.size() - 1 : 1;
+    for (int64_t i = 0; i < std::min<int64_t>(capacity, info->n_chunks + 1); ++i)
+        chunk_rows[i] = chunked ? p->chunk_rows[(size_t)i] : (i == 0 ? 0 : p->A.rows);
+    return SPG_STATUS_SUCCESS;
+}
+
 spg_status_t spg_plan_destroy(spg_plan_t p) {
     if (!p) return SPG_STATUS_INVALID_VALUE;
     delete p;

@@ -294,5 +294,31 @@ def num_products(a: csr_matrix, b: csr_matrix) -> int:
         h.lib.spg_plan_destroy(plan)
 
 
+def plan_info(a: csr_matrix, b: csr_matrix, alg: int = 0, chunk_fraction: float = 0.2) -> dict:
+    """What spgemm(a, b, alg, chunk_fraction) runs (spg_plan_info): the kernel path, the
+    tile geometry and the row chunks (ALG3's chunk cut).  A diagnostic for tests/profilers."""
+    h = _handle_for(a)
+    va, vb = _csr_view(a), _csr_view(b)
+    algo = _ALG.get(alg, _lib.SPG_ALG_DEFAULT)
+    ws_bytes = ctypes.c_size_t(0)
+    check(h.lib.spg_plan(h.ptr, ctypes.byref(va), ctypes.byref(vb), algo, float(chunk_fraction),
+                         ctypes.byref(ws_bytes), None, None), "spg_plan")
+    ws = torch.empty(max(ws_bytes.value, 1), dtype=torch.uint8, device=a.device)
+    plan = ctypes.c_void_p()
+    check(h.lib.spg_plan(h.ptr, ctypes.byref(va), ctypes.byref(vb), algo, float(chunk_fraction),
+                         ctypes.byref(ws_bytes), ctypes.c_void_p(ws.data_ptr()), ctypes.byref(plan)), "spg_plan")
+    try:
+        info = _lib.SpgPlanInfo()
+        check(h.lib.spg_plan_info(plan, ctypes.byref(info), None, 0), "spg_plan_info")
+        rows = (ctypes.c_int64 * (info.n_chunks + 1))()
+        check(h.lib.spg_plan_info(plan, ctypes.byref(info), rows, info.n_chunks + 1), "spg_plan_info")
+        return {"path": ("general", "short", "tile")[info.path], "tile_width": info.tile_width,
+                "tiles_per_row": info.tiles_per_row, "dense_tiles": bool(info.dense_tiles),
+                "chunk_rows": [int(x) for x in rows]}
+    finally:
+        h.lib.spg_plan_destroy(plan)
+        torch.cuda.current_stream(a.device).synchronize()
+
+
 __all__ = ["spgemm", "spmv", "check_availability", "num_products", "validate_csr", "SpgError",
            "last_stats"]

@@ -4,13 +4,15 @@
   density 1e-2 and 1e-1 (ALG2), bit-exact against the CPU oracle over every row (the OpenMP
   oracle for 1e-1: 5.5e9 products).
 * Config 4 (N = 65536, density 5e-3, ALG3 chunked): nnz(C) = 3.46e9 needs an int64 row
-  pointer.  256 sampled rows bit-exact against the oracle, plus size-independent properties
+  pointer.  >= 2048 stratified rows bit-exact against the oracle (the first and last rows of
+  every ALG3 chunk, the longest A and C rows, rows with a tile item past one accumulator
+  window, uniform fill), plus size-independent properties
   over the whole result: int64 row pointer, monotone, row_ptr[-1] = nnz(C) within the
   analytic expectation, every row's columns strictly increasing and in range, no row longer
   than its product count or N, and P (getNumProducts) equal to sum over A's entries of the
   B row lengths.
-* Config 5 on one GPU (N = 262144, density 1e-3, ALG2): the same checks (200 GB of C and
-  workspace fit the 288 GB of one MI355X).
+* Config 5 on one GPU (N = 262144, density 1e-3, ALG2 and ALG3): the same checks (200 GB of
+  C and workspace fit the 288 GB of one MI355X).
 * ALG3's working-set cap on a sparse-tile shape: peak bytes fall as chunk_fraction falls,
   with bit-identical results; on dense tiles ALG3 stays within ALG2's peak.
 
@@ -63,8 +65,9 @@ def _expected_nnz(a_lens, n, density):
 
 
 @torch.no_grad()
-def _check_structure(A, B, C, n, density):
-    """Size-independent properties of C over every row (device-side, in row chunks)."""
+def _check_structure(A, B, C, n, density, tile_width):
+    """Size-independent properties of C over every row (device-side, in row chunks).
+    Returns (P, per-row nnz(C) on the host, rows with a tile item over TILE_CAP entries)."""
     m = A.shape[0]
     p = C.indptr
     assert p.dtype == torch.int64, "nnz(C) >= 2^31 needs an int64 row pointer"
@@ -81,7 +84,9 @@ def _check_structure(A, B, C, n, density):
     # nnz(C) against its expectation (relative std ~1e-5 at these sizes)
     exp = _expected_nnz((A.indptr[1:] - A.indptr[:-1]).cpu().numpy(), n, density)
     assert abs(C.nnz - exp) / exp < 2e-3, (C.nnz, exp)
-    # columns in range and strictly increasing inside every row
+    # columns in range and strictly increasing inside every row; entries per (row, tile)
+    G = (n + tile_width - 1) // tile_width
+    over_cap = []
     step = max(1, int(4e8 // max(1, C.nnz // m)))   # ~4e8 entries per chunk
     for r0 in range(0, m, step):
         r1 = min(m, r0 + step)
@@ -95,37 +100,90 @@ def _check_structure(A, B, C, n, density):
         start[(p[r0:r1] - s)[lens[r0:r1] > 0]] = True
         ok = (cols[1:] > cols[:-1]) | start[1:]
         assert bool(ok.all()), f"columns not increasing in rows [{r0}, {r1})"
-        del cols, start, ok
-    return int(P_i.sum())
+        rid = torch.repeat_interleave(torch.arange(r1 - r0, device=cols.device), lens[r0:r1])
+        items = torch.bincount(rid * G + (cols // tile_width).to(torch.int64), minlength=(r1 - r0) * G)
+        big = torch.nonzero(items.view(r1 - r0, G).max(dim=1).values > TILE_CAP).flatten() + r0
+        over_cap.append(big.cpu().numpy())
+        del cols, start, ok, rid, items
+    return int(P_i.sum()), lens.cpu().numpy(), np.concatenate(over_cap) if over_cap else np.zeros(0, np.int64)
 
 
-def _sampled_bitexact(A, B, C, nrows, seed=0):
+TILE_CAP = 1024   # entries of one tile-item accumulator window (spgemm_tile.hpp)
+
+
+def _stratified_rows(A, C_lens, chunk_rows, over_cap, total=2048, seed=0):
+    """Rows where the schedule changes, then uniform ones up to `total`:
+    * the first and last row of every row chunk (ALG3's chunk cut) and their neighbours;
+    * the longest A rows and the largest C rows;
+    * rows with a tile item past TILE_CAP entries (windowed items, sparse tiles);
+    * the first and last rows of the matrix."""
+    m = A.shape[0]
+    a_lens = (A.indptr[1:] - A.indptr[:-1]).cpu().numpy()
+    pick = set()
+    for r in chunk_rows:
+        for d in (-2, -1, 0, 1):
+            if 0 <= r + d < m:
+                pick.add(r + d)
+    pick.update(np.argsort(a_lens)[-32:].tolist())
+    pick.update(np.argsort(C_lens)[-32:].tolist())
+    pick.update(np.argsort(C_lens)[:16].tolist())
     rng = np.random.default_rng(seed)
-    rows = np.sort(rng.choice(A.shape[0], size=nrows, replace=False))
+    if len(over_cap):
+        pick.update(rng.choice(over_cap, size=min(len(over_cap), 512), replace=False).tolist())
+    pick.update([0, 1, m - 2, m - 1])
+    rest = np.setdiff1d(np.arange(m), np.fromiter(pick, np.int64))
+    pick.update(rng.choice(rest, size=max(0, total - len(pick)), replace=False).tolist())
+    return np.array(sorted(pick), dtype=np.int64)
+
+
+@torch.no_grad()
+def _sampled_bitexact(A, B, C, rows):
+    """The sampled rows of C against the oracle on the same rows of A (all of B), bit for bit:
+    the rows' entries gathered on the device in one index op, one copy to the host."""
     Ah, Bh = A.get(), B.get()
     rp, rj, rx = oracle.spgemm(sp.csr_matrix(Ah[rows]), Bh, keep_zeros=True, sort=True, threads=THREADS)
-    p = C.indptr.cpu().numpy()
-    for q, i in enumerate(rows):
-        s, e = int(p[i]), int(p[i + 1])
-        assert e - s == rp[q + 1] - rp[q], f"row {i}: nnz"
-        assert np.array_equal(C.indices[s:e].cpu().numpy(), rj[rp[q]:rp[q + 1]]), f"row {i}: columns"
-        assert np.array_equal(_bits(C.data[s:e].cpu().numpy()), _bits(rx[rp[q]:rp[q + 1]])), f"row {i}: values"
+    p = C.indptr
+    tr = torch.from_numpy(rows).to(p.device)
+    s, e = p[tr], p[tr + 1]
+    got_lens = (e - s).cpu().numpy()
+    bad = np.nonzero(got_lens != np.diff(rp))[0]
+    assert len(bad) == 0, f"nnz differs in rows {rows[bad[:8]].tolist()}"
+    idx = torch.repeat_interleave(s, e - s) + (torch.arange(int((e - s).sum()), device=p.device)
+                                               - torch.repeat_interleave(torch.cumsum(e - s, 0) - (e - s), e - s))
+    gj = C.indices[idx].cpu().numpy()
+    gx = C.data[idx].cpu().numpy()
+    if not np.array_equal(gj, rj):
+        q = int(np.searchsorted(rp, int(np.nonzero(gj != rj)[0][0]), side="right") - 1)
+        raise AssertionError(f"row {rows[q]}: columns")
+    if not np.array_equal(_bits(gx), _bits(rx)):
+        q = int(np.searchsorted(rp, int(np.nonzero(_bits(gx) != _bits(rx))[0][0]), side="right") - 1)
+        raise AssertionError(f"row {rows[q]}: values")
 
 
 @pytest.mark.parametrize("n,density,alg,cf,expect_products", [
     (65536, 5e-3, 3, 0.2, 7.04e9),     # config 4
     (262144, 1e-3, 2, 0.2, 1.80e10),   # config 5, one GPU
+    (262144, 1e-3, 3, 0.2, 1.80e10),   # config 5, ALG3 chunked (sparse tiles cap the working set)
 ])
-def test_large_config_sampled_and_properties(n, density, alg, cf, expect_products):
+def test_large_config_stratified_and_properties(n, density, alg, cf, expect_products):
+    """Configs 4 and 5 at full size: whole-result properties over every row, and >= 2048
+    stratified rows (ALG3 chunk boundaries, extreme A/C rows, windowed tile items, uniform
+    fill) bit-exact against the oracle."""
     from spmm_amd import cusparse, gen
     A = gen.random_csr(n, n, density, seed=42, device=DEV)
     B = gen.random_csr(n, n, density, seed=43, device=DEV)
+    info = cusparse.plan_info(A, B, alg=alg, chunk_fraction=cf)
+    assert info["path"] == "tile"
+    if alg == 3:
+        assert len(info["chunk_rows"]) - 1 >= 5, info   # chunk_fraction 0.2: >= 5 chunks
     C = cusparse.spgemm(A, B, alg=alg, chunk_fraction=cf)
     torch.cuda.synchronize()
-    P = _check_structure(A, B, C, n, density)
+    P, C_lens, over_cap = _check_structure(A, B, C, n, density, info["tile_width"])
     assert P == cusparse.num_products(A, B)
     assert abs(P - expect_products) / expect_products < 0.02
-    _sampled_bitexact(A, B, C, 256)
+    rows = _stratified_rows(A, C_lens, info["chunk_rows"], over_cap)
+    assert len(rows) >= 2048
+    _sampled_bitexact(A, B, C, rows)
     del C
     torch.cuda.empty_cache()
 
