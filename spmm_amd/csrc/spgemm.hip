@@ -19,6 +19,7 @@
 #include "spgemm.h"
 #include "spgemm_kernels.hpp"
 #include "spgemm_tile.hpp"
+#include "spgemm_tile_dn.hpp"
 #include "spgemm_spmv.hpp"
 #include "spgemm_row.hpp"
 
@@ -35,6 +36,11 @@ struct spg_handle_s {
     int64_t mirror_gen = 0;         // generation of the last scan that mirrors into `pinned`
     int32_t* spill_ctr = nullptr;   // ALG1 on k_row: spill counter, re-armed by the scan kernel
     bool spill_ctr_dirty = false;   // a count pass ran without its scan (re-zero first)
+    // bound of the ALG1 numeric launch's waits (scan look-back, 64-row group words), wall-clock
+    // ticks; a wait past it computes the prefix directly (same result).  SPG_LB_SPIN_TICKS
+    // (read once per handle) lowers it -- 0 sends every wait to that path, which the GPU
+    // tests use to check it bit for bit; it cannot change any result.
+    uint64_t lb_spin = SCAN_SPIN;
     void* scratch = nullptr;        // internal device scratch (plan-time analysis)
     size_t scratch_bytes = 0;
     // per-phase timing (spg_set_timing / spg_get_timing)
@@ -80,6 +86,7 @@ struct spg_plan_s {
     int G = 1;                      // tiles per row
     int TR = 1;                     // tiles per wave task (a run of one row's tiles)
     int twss = 10;                  // log2 of the symbolic tile width (>= tws, <= 16)
+    bool sym_seg = false;           // symbolic tiles by the segment-walking kernel (long segments)
     bool counts_ready = false;      // a symbolic pass has completed (counts / offsets valid)
     unsigned long long* lb = nullptr;   // ALG1 single pass: per-row look-back status words
     void* ext = nullptr;            // ALG1 on k_row: every A entry's B row extent (RowExt)
@@ -122,13 +129,18 @@ inline size_t vbytes(spg_dtype_t t) {
 inline size_t brec_bytes(spg_dtype_t t) { return 4 + vbytes(t); }
 
 // Runs f(T{}) with T the C++ type of value type t.
+// (SPG_ONLY_F64: fp64-only development builds for A/B timing, about 3x faster to compile;
+// never shipped -- the other value types then return NOT_SUPPORTED.)
 template <typename F>
 spg_status_t dispatch_value(spg_dtype_t t, F&& f) {
     switch (t) {
+#ifndef SPG_ONLY_F64
         case SPG_R_32F: return f(float(0));
-        case SPG_R_64F: return f(double(0));
         case SPG_C_32F: return f(cplx<float>(0));
         case SPG_C_64F: return f(cplx<double>(0));
+#endif
+        case SPG_R_64F: return f(double(0));
+        default: break;
     }
     return SPG_STATUS_NOT_SUPPORTED;
 }
@@ -159,6 +171,11 @@ inline bool row_kernel_enabled() {
 #ifndef SPG_TILE_TWS
 #define SPG_TILE_TWS 0
 #endif
+//   SPG_TILE_LEAN   0 keeps the owner-round k_tile on dense tiles (A/B against k_tile_dn)
+#ifndef SPG_TILE_LEAN
+#define SPG_TILE_LEAN 1
+#endif
+
 struct TileVariant { int ru; bool dense; };
 inline const TileVariant& tile_variant() {
     static const TileVariant v{SPG_TILE_RU, SPG_TILE_DENSE != 0};
@@ -212,9 +229,17 @@ inline unsigned tile_grid(int64_t tasks, int wpb = TILE_WPB) {
 
 // symbolic tile: the narrowest width >= the numeric tile whose B segments (expected B row
 // entries per tile) reach 64 entries -- long coalesced reads -- capped at 65536 columns
-// and at the (pow2-rounded) row width
-inline int sym_tile_log2(const spg_csr_t& B, int tws) {
+// and at the (pow2-rounded) row width.  When the widest symbolic tile (65536 columns or the
+// whole row) holds segments of >= SEG_MIN entries, that width and the segment-walking
+// symbolic kernel (k_tile_sym_seg) are used instead.
+constexpr double SEG_MIN = 160.0;
+inline int sym_tile_log2(const spg_csr_t& B, int tws, bool* seg = nullptr) {
     const double avgB = B.rows > 0 ? (double)B.nnz / (double)B.rows : 0.0;
+    int tmax = tws;
+    while (tmax < 16 && ((int64_t)1 << tmax) < B.cols) ++tmax;
+    const double seg_max = avgB * std::min(1.0, (double)((int64_t)1 << tmax) / (double)std::max<int64_t>(B.cols, 1));
+    if (seg) *seg = seg_max >= SEG_MIN;
+    if (seg_max >= SEG_MIN) return tmax;
     int t = tws;
     while (t < 16 && ((int64_t)1 << t) < B.cols && avgB * (double)((int64_t)1 << t) / (double)B.cols < 64.0) ++t;
     return t;
@@ -794,10 +819,16 @@ spg_status_t tile_sym_chunk(spg_handle_t h, spg_plan_s& p, int64_t c) {
     const int64_t r0 = tile_chunk_r0(p, c), n = tile_chunk_r1(p, c) - r0;
     int64_t* items = tile_chunk_items(p, c);
     if (n > 0) {
-        timed_launch(h, SPG_PHASE_SYMBOLIC, k_tile_sym<IP>, dim3(tile_grid(n * sym_tiles(p))), dim3(TILE_WPB * WAVE),
-                           r0, n, p.tws, p.G, p.twss, (const IP*)p.A.indptr, (const int32_t*)p.A.indices,
-                           (const IP*)p.B.indptr, (const int32_t*)p.B.indices, (const uint32_t*)p.sidx,
-                           tile_dense(p) ? (uint32_t*)nullptr : p.bitmap, items);
+        if (p.sym_seg)
+            timed_launch(h, SPG_PHASE_SYMBOLIC, k_tile_sym_seg<IP>, dim3(tile_grid(n * sym_tiles(p), SEG_WPB)),
+                         dim3(SEG_WPB * WAVE), r0, n, p.tws, p.G, p.twss, (const IP*)p.A.indptr,
+                         (const int32_t*)p.A.indices, (const IP*)p.B.indptr, (const int32_t*)p.B.indices,
+                         (const uint32_t*)p.sidx, tile_dense(p) ? (uint32_t*)nullptr : p.bitmap, items);
+        else
+            timed_launch(h, SPG_PHASE_SYMBOLIC, k_tile_sym<IP>, dim3(tile_grid(n * sym_tiles(p))), dim3(TILE_WPB * WAVE),
+                         r0, n, p.tws, p.G, p.twss, (const IP*)p.A.indptr, (const int32_t*)p.A.indices,
+                         (const IP*)p.B.indptr, (const int32_t*)p.B.indices, (const uint32_t*)p.sidx,
+                         tile_dense(p) ? (uint32_t*)nullptr : p.bitmap, items);
         SPG_LAUNCHED(h);
     }
     const int64_t nch = tile_chunks(p);
@@ -874,6 +905,16 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
                                   dense ? (const uint32_t*)nullptr : (const uint32_t*)p.bitmap,
                                   (const int64_t*)tile_chunk_items(p, c), cj, cx, alpha);
         };
+        if constexpr (OrderedLdsAdd<T>::value) {
+            if (dense && SPG_TILE_LEAN) {   // ordered LDS adds (spgemm_tile_dn.hpp)
+                hipExtLaunchKernelGGL((k_tile_dn<T, IP>), dim3(tile_grid(n * p.G, DN_WPB)), dim3(DN_WPB * WAVE), 0,
+                                      h->stream, kt.a, kt.b, 0, r0, n, p.tws, p.G, Ap, Aj, Ax, p.B.rows,
+                                      (const uint32_t*)p.brec, (const int32_t*)p.tptr,
+                                      (const int64_t*)tile_chunk_items(p, c), cj, cx, alpha);
+                SPG_LAUNCHED(h);
+                continue;
+            }
+        }
         constexpr int UF = sizeof(T) > 8 ? 4 : 8;
         using D1 = std::integral_constant<bool, true>;
         using D0 = std::integral_constant<bool, false>;
@@ -906,7 +947,8 @@ spg_status_t alg1_fused_run(spg_handle_t h, spg_plan_s& p, void* cp) {
         const int64_t nscan = scan_tiles(p.A.rows);
         const int64_t nstatus = nscan + 1 + row_groups(p.A.rows);
         RowExt<IP>* ext = (RowExt<IP>*)p.ext;
-        RowScan<OUT> sa{nscan, (OUT*)cp, status, status + nscan + 1, p.scalars, nullptr, nullptr, nullptr, 0, 0};
+        RowScan<OUT> sa{nscan, (OUT*)cp, status, status + nscan + 1, p.scalars, nullptr, nullptr, nullptr, 0, 0,
+                        h->lb_spin};
         if (!p.counts_ready) {
             if (h->spill_ctr_dirty) SPG_HIP(h, hipMemsetAsync(h->spill_ctr, 0, sizeof(int32_t), h->stream));
             h->spill_ctr_dirty = true;
@@ -1099,6 +1141,7 @@ spg_status_t spg_create(spg_handle_t* handle, int hip_device) {
     if (!h) return SPG_STATUS_ALLOC_FAILED;
     h->device = dev;
     h->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    if (const char* e = std::getenv("SPG_LB_SPIN_TICKS")) h->lb_spin = std::strtoull(e, nullptr, 10);
     DeviceGuard dg_(dev);   // the handle's allocations on its device; the caller's device stays current
     hipError_t e = dg_.err;
     // fine-grained (coherent) host memory: the scan's system-scope stores of the scalars and
@@ -1168,7 +1211,7 @@ spg_status_t spg_plan(spg_handle_t h, const spg_csr_t* A, const spg_csr_t* B, sp
     tmp.use_tile = !tmp.use_short && want_tile(*A, *B, tmp.tws, tmp.G);
     if (tmp.use_tile) {
         tmp.TR = 1;
-        tmp.twss = sym_tile_log2(*B, tmp.tws);
+        tmp.twss = sym_tile_log2(*B, tmp.tws, &tmp.sym_seg);
     }
     // spills are rare for the shapes the short kernel is chosen for (A rows > 64 entries or
     // C wider than 16384 columns): a small grid keeps the usually-empty launch cheap
@@ -1198,8 +1241,28 @@ spg_status_t spg_plan(spg_handle_t h, const spg_csr_t* A, const spg_csr_t* B, sp
             tmp.chunk_rows = h->q_chunk_rows;
             tmp.chunk_nz = h->q_chunk_nz;
             tmp.seg_len = h->q_seg_len;
-        } else if ((st = plan_chunks(h, tmp))) {
-            return st;
+        } else {
+            if ((st = plan_chunks(h, tmp))) return st;
+            // The ALG3 cap: chunk_fraction of the single-pass (ALG1) buffer, P entries of
+            // C's (index, value) pairs -- the working set cuSPARSE's ALG3 trades time against
+            // (estimateMemory, spgemm_from_txt_alg3.cu:195-202).  When the unchunked
+            // workspace is already within it, chunking would only add launches: one chunk.
+            spg_plan_s whole = tmp;
+            whole.chunk_rows.assign({0, A->rows});
+            whole.chunk_nz.assign({0, A->nnz});
+            whole.seg_len = A->nnz;
+            if (tmp.use_tile) whole.seg_len = 1;
+            const double cap = (double)chunk_fraction * (double)std::max<int64_t>(tmp.P, 0) *
+                               (double)(sizeof(int32_t) + vbytes(A->value_type));
+            // (SPG_ALG3_CHUNK_ALWAYS=1 keeps the chunks regardless: a schedule-only switch the
+            // GPU tests use to cover the chunked paths on small inputs; results are identical)
+            const char* ae = std::getenv("SPG_ALG3_CHUNK_ALWAYS");
+            const bool always = ae && std::strcmp(ae, "1") == 0;
+            if (!always && tmp.chunk_rows.size() > 2 && (double)make_layout(whole).total <= cap) {
+                tmp.chunk_rows = whole.chunk_rows;
+                tmp.chunk_nz = whole.chunk_nz;
+                tmp.seg_len = whole.seg_len;
+            }
         }
     }
     if (tmp.use_tile) tmp.seg_len = 1;   // no cursor scratch on the tile path

@@ -760,13 +760,30 @@ struct ScanLds {
 // status words (status + 1).  With `gpre`, the exclusive prefix at every 64-element group
 // start also goes to gpre[group] | GPRE_READY (agent-scope stores: k_row's ALG1 numeric
 // pass reads its rows' offsets from them while the scan runs beside it).
+// Bounded waits: a look-back that finds a predecessor's status word still
+// empty after SCAN_SPIN wall-clock ticks (100 MHz: 2 ms) stops waiting and computes what it
+// waited for directly from the inputs -- the exclusive prefix is the sum of in[0 .. base),
+// all of which are in memory before the launch -- so the result is the same and the grid
+// drains even if a predecessor tile were never scheduled (a dispatch order the ticket
+// scheme already rules out).  The same bound guards k_row's wait on the 64-row group words.
+constexpr uint64_t SCAN_SPIN = 200000;
+
+// sum of in[0 .. n) over one wave (the fallback of a timed-out wait; never the fast path)
+template <typename IN>
+__device__ __forceinline__ long long wave_direct_sum(const IN* in, int64_t n) {
+    long long s = 0;
+    for (int64_t i = lane_id(); i < n; i += WAVE) s += (long long)in[i];
+    return wave_sum64(s);
+}
+
 template <typename OUT, typename IN>
 __device__ __forceinline__ void scan_tile(int64_t bid, int64_t n, const IN* in, OUT* out,
                                           unsigned long long* __restrict__ st, int64_t* __restrict__ scalars,
                                           int32_t* __restrict__ move_cnt, int64_t* __restrict__ move_dst,
                                           int64_t* __restrict__ host_mirror, int64_t mirror_gen, int mirror_n,
                                           const int64_t* seed, ScanLds& L,
-                                          unsigned long long* __restrict__ gpre = nullptr) {
+                                          unsigned long long* __restrict__ gpre = nullptr,
+                                          uint64_t spin = SCAN_SPIN) {
     static_assert(SCAN_ITEMS * 8 == WAVE, "8 threads per 64-element group");
     constexpr unsigned long long VMASK = SCAN_VMASK;
     long long* wsum = L.wsum;
@@ -801,14 +818,21 @@ __device__ __forceinline__ void scan_tile(int64_t bid, int64_t n, const IN* in, 
                 __hip_atomic_store(&st[bid], (1ull << 62) | (unsigned long long)btot, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
             int64_t j = bid - 1;
-            for (;;) {
+            const uint64_t t0 = wall_clock64();
+            bool late = spin == 0;   // (spin 0: the direct path, for the tests)
+            for (; !late;) {
                 const int64_t q = j - l;
                 unsigned long long s = 0;
                 if (q >= 0) {
                     do {
                         s = __hip_atomic_load(&st[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if ((s >> 62) == 0 && wall_clock64() - t0 > spin) {
+                            s = 2ull << 62;   // stop waiting (the direct sum below replaces the prefix)
+                            late = true;
+                        }
                     } while ((s >> 62) == 0);
                 }
+                if (__ballot(late)) break;
                 const unsigned long long incm = __ballot(q >= 0 && (s >> 62) == 2);
                 const int stop = incm ? __ffsll((long long)incm) - 1 : WAVE;
                 const long long val = (q >= 0 && l <= stop) ? (long long)(s & VMASK) : 0;
@@ -816,6 +840,7 @@ __device__ __forceinline__ void scan_tile(int64_t bid, int64_t n, const IN* in, 
                 if (incm || j - WAVE < 0) break;
                 j -= WAVE;
             }
+            if (__ballot(late)) prefix = (seed ? *seed : 0) + wave_direct_sum(in, bid * SCAN_TILE);
             if (l == 0)
                 __hip_atomic_store(&st[bid], (2ull << 62) | (unsigned long long)(prefix + btot),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -189,13 +189,21 @@ template <typename OFF> struct RowScan {
     int64_t* host_mirror;
     int64_t mirror_gen;
     int mirror_n;
+    uint64_t spin;                     // bound of every wait, wall-clock ticks (SCAN_SPIN)
 };
 
-// the exclusive prefix of a row group: its published word (the scan blocks were dispatched
-// before every row block and wait on nothing the row blocks produce, so it arrives); the
-// wait stays in scalar registers (the row's output occupies the vector registers)
-__device__ __forceinline__ long long row_group_prefix(const unsigned long long* gp, unsigned long long gw) {
+// the exclusive prefix of a row group: its published word.  The scan tiles take tickets in
+// the order they start and wait on nothing the row blocks produce, so the word arrives; a
+// wait past `spin` ticks (a scan tile not scheduled, which no dispatch order should cause)
+// stops and sums the group's preceding row counts directly -- same value, and the wave
+// always finishes.  The wait stays in scalar registers (the row's output occupies the vector
+// registers).
+__device__ __forceinline__ long long row_group_prefix(const unsigned long long* gp, unsigned long long gw,
+                                                      const int64_t* cnt, int64_t g0, uint64_t spin) {
+    if (spin == 0) return wave_direct_sum(cnt, g0);   // (the direct path, for the tests)
+    const uint64_t t0 = wall_clock64();
     while (!(gw & GPRE_READY)) {
+        if (wall_clock64() - t0 > spin) return wave_direct_sum(cnt, g0);
         __builtin_amdgcn_s_sleep(2);
         const unsigned long long v = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         gw = ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
@@ -551,10 +559,15 @@ __global__ __launch_bounds__(G::WPB * WAVE, sizeof(T) <= 8 ? 5 : 3) void k_row(
         for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < nzero; i += (int64_t)gridDim.x * BLOCK)
             zero_words[i] = 0ull;
     if (lb && (int64_t)blockIdx.x < sa.nscan) {
+        // a scan block scans the tile of the ticket it takes (tickets follow the order the
+        // scan blocks start, so every tile's predecessors have started: the look-back ends)
         __shared__ ScanLds scan_l;
-        scan_tile<OFF, int64_t>(blockIdx.x, nrows, row_cnt + row0, sa.out, sa.status + 1, sa.scalars,
+        __shared__ int64_t ticket;
+        if (threadIdx.x == 0) ticket = (int64_t)atomicAdd(&sa.status[0], 1ull);
+        __syncthreads();
+        scan_tile<OFF, int64_t>(ticket, nrows, row_cnt + row0, sa.out, sa.status + 1, sa.scalars,
                                 sa.move_cnt, sa.move_dst, sa.host_mirror, sa.mirror_gen, sa.mirror_n,
-                                nullptr, scan_l, sa.gpre);
+                                nullptr, scan_l, sa.gpre, sa.spin);
         return;
     }
     const int l = lane_id();
@@ -635,7 +648,8 @@ __global__ __launch_bounds__(G::WPB * WAVE, sizeof(T) <= 8 ? 5 : 3) void k_row(
                     const unsigned long long g = S.lb_gw;   // (all lanes read the same word)
                     base = row_group_prefix(&sa.gpre[it >> 6],
                                             ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(g >> 32)) << 32) |
-                                                (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)g)) +
+                                                (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)g),
+                                            row_cnt + row0, it & ~(int64_t)(WAVE - 1), sa.spin) +
                            __builtin_amdgcn_readfirstlane((int)S.lb_gsum);
                     const int64_t end = base + nnz;
                     room = (cap <= 0 || end <= cap) && (sizeof(OFF) == 8 || end <= 2147483647LL);

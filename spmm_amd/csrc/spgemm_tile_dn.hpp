@@ -1,0 +1,304 @@
+// spgemm_tile_dn.hpp -- lean kernels of the tile path (dense numeric tiles, long-segment
+// symbolic tiles).
+//
+// Ordered accumulation by LDS atomic add.  Two properties of gfx950's LDS, measured on
+// MI355X by abtest/lds_fadd_order.hip (4.2M operand pairs incl. denormals, +-0, inf, nan;
+// 50,000 wave instructions with 1.4M same-address lane pairs, every trial bit-exact):
+//   * ds_add_f64 rounds exactly like v_add_f64 (IEEE round-to-nearest-even, denormals kept);
+//   * the lanes of ONE ds_add_f64 that hit the same address are applied in ascending lane
+//     order, and the DS instructions of a wave execute in issue order.
+// So if the products of an item are laid out in flattened (jj, kk) order -- A entry
+// jj ascending, then the entry's B segment -- 64 per instruction, one `ds_add_f64` per
+// 64-product chunk performs every C(i,j) sum in scipy's order: two products of the same
+// column come from different A entries, the earlier one sits in an earlier chunk or a lower
+// lane of the same chunk.  That replaces the owner-tag rounds of k_tile (a ds_min, a read
+// back, a read-add-write and a retry loop per chunk) with one fire-and-forget LDS op.  The
+// GPU parity tests re-check the property end to end on every run (bit-exact vs the oracle).
+#pragma once
+
+#include "spgemm_tile.hpp"
+
+namespace spg {
+
+// LDS atomic add with the ordering property above (f64 parts only; f32 parts keep k_tile).
+template <typename T> struct OrderedLdsAdd : std::false_type {};
+template <> struct OrderedLdsAdd<double> : std::true_type {};
+template <> struct OrderedLdsAdd<cplx<double>> : std::true_type {};
+
+__device__ __forceinline__ void lds_add(double* p, double v) {
+    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_add(cplx<double>* p, cplx<double> v) {
+    lds_add(&p->re, v.re);
+    lds_add(&p->im, v.im);
+}
+
+constexpr int DN_TW = 1024;   // dense tiles: <= TILE_CAP columns, one accumulator window
+constexpr int DN_WPB = 2;     // waves per block
+
+// Per-batch A-entry table: the byte offset of the entry's first product record, shifted by
+// the entry's flattened offset (so product t of the batch reads base[src] + t * RB), and the
+// A value.  One 16-byte LDS read per product lane (f64).
+template <typename T> struct __attribute__((aligned(16))) DnEnt {
+    uint32_t base;
+    uint32_t pad;
+    T a;
+};
+
+template <typename T> struct DnLds {
+    T acc[DN_TW + WAVE];          // accumulator by column; + one lane-private slot per lane
+    DnEnt<T> ent[WAVE];
+    uint8_t hit[DN_TW + WAVE];    // columns some product reached (the item's structure)
+    uint8_t mk[NUM_MK];           // lane -> A-entry markers of 8 chunks
+};
+
+// Numeric pass on dense tiles (TW <= 1024 columns): one wave per (row, tile) item, items
+// tile-major over the XCD-aware block map (as k_tile).  Per batch of 64 A entries: each lane's
+// entry, value and tile segment (the first NB batches preloaded); a DPP scan of the segment
+// lengths; the entry table in LDS.  Per group of 8 chunks the transposed markers; per U
+// chunks: the lane -> entry max-scans, one table read and one record load per chunk (all in
+// flight), then per chunk in order one multiply, one ds_add_f64 into acc[column] and one byte
+// store into hit[column].  Lanes past the batch's products add 0 into their own private
+// slot.  The item's output: 64 columns at a time from hit[] (ballot + lane rank give
+// positions), straight to C at its offset.
+template <typename T, typename IP>
+__global__ __launch_bounds__(DN_WPB * WAVE) void k_tile_dn(
+    int64_t row0, int64_t nrows, int tws, int G, const IP* __restrict__ Ap,
+    const int32_t* __restrict__ Aj, const T* __restrict__ Ax, int64_t K,
+    const uint32_t* __restrict__ brec, const int32_t* __restrict__ tptr,
+    const int64_t* __restrict__ item_off, int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha) {
+    static_assert(OrderedLdsAdd<T>::value, "ordered LDS add needed");
+    constexpr int U = sizeof(T) > 8 ? 4 : 8;     // chunks in flight
+    constexpr int NB = sizeof(T) > 8 ? 4 : 8;    // A batches preloaded per item
+    constexpr uint32_t RB = 4u * (uint32_t)rec_words<T>();   // bytes of one B record
+    __shared__ __attribute__((aligned(16))) DnLds<T> lds[DN_WPB];
+    const int l = lane_id();
+    const int wv = uniform((int)(threadIdx.x >> 6));
+    DnLds<T>& S = lds[wv];
+    const int TW = 1 << tws;
+    const char* __restrict__ rb = reinterpret_cast<const char*>(brec);
+    const uint32_t items = (uint32_t)(nrows * G);   // host keeps rows*G < 2^31
+    for (uint32_t it = xcd_block(gridDim.x) * DN_WPB + wv; it < items; it += gridDim.x * DN_WPB) {
+        const int g = (int)(it / (uint32_t)nrows);
+        const int64_t row = row0 + (int64_t)(it - (uint32_t)g * (uint32_t)nrows);
+        const int64_t item = (row - row0) * G + g;
+        const int64_t obase = item_off[item];
+        const int nnz = (int)(item_off[item + 1] - obase);
+        if (nnz == 0) continue;                      // (no product reaches this tile)
+        const int32_t* __restrict__ tp = tptr + (int64_t)g * (K + 1);
+        const int64_t a0 = Ap[row];
+        const int nA = (int)(Ap[row + 1] - a0);
+        // the first NB batches' A entries, values and tile segments, loaded up front
+        int32_t kq[NB];
+        T aq[NB];
+        uint2 sq[NB];
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+            kq[q] = -1;
+            aq[q] = (T)0;
+            if (q * WAVE + l < nA) {
+                kq[q] = Aj[a0 + q * WAVE + l];
+                aq[q] = Ax[a0 + q * WAVE + l];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+            sq[q] = make_uint2(0u, 0u);
+            if (kq[q] >= 0) sq[q] = seg_pair(tp, kq[q]);
+        }
+        wsync();
+        {   // clear the accumulator and the hit bytes (16-byte stores; TW is a multiple of 64)
+            uint4* a4 = reinterpret_cast<uint4*>(S.acc);
+            for (int q = l; q < TW * (int)sizeof(T) / 16; q += WAVE) a4[q] = make_uint4(0u, 0u, 0u, 0u);
+            uint4* h4 = reinterpret_cast<uint4*>(S.hit);
+            for (int q = l; q < TW / 16; q += WAVE) h4[q] = make_uint4(0u, 0u, 0u, 0u);
+        }
+        for (int b = 0; b < nA; b += WAVE) {
+            int cnt = 0;
+            uint32_t beg = 0;
+            T av = (T)0;
+            if (b < NB * WAVE) {
+#pragma unroll
+                for (int q = 0; q < NB; ++q)
+                    if (q == (b >> 6)) {
+                        cnt = (int)(sq[q].y - sq[q].x);
+                        beg = sq[q].x;
+                        av = aq[q];
+                    }
+            } else if (b + l < nA) {
+                const uint2 se = seg_pair(tp, Aj[a0 + b + l]);
+                cnt = (int)(se.y - se.x);
+                beg = se.x;
+                av = Ax[a0 + b + l];
+            }
+            const int incl = wave_incl_sum_dpp(cnt);
+            const int off = incl - cnt;
+            const int Pb = readlane_i(incl, WAVE - 1);
+            wsync();
+            S.ent[l].base = beg * RB - (uint32_t)off * RB;   // wraps; base + t*RB is exact
+            S.ent[l].a = av;
+            unsigned carry = 0u;
+            for (int gb = 0; gb < Pb; gb += NUM_MK) {
+                num_group_markers(S, l, cnt, off, gb);
+                const int nchg = min(NUM_MK, Pb - gb);
+                const uint2 m2 = reinterpret_cast<const uint2*>(S.mk)[l];
+                const uint64_t mrow = ((uint64_t)m2.y << 32) | m2.x;
+                for (int c0 = 0; c0 < nchg; c0 += U * WAVE) {
+                    const int nu = min(U, (nchg - c0 + WAVE - 1) >> 6);
+                    auto step = [&](auto nuc) {
+                        constexpr int NU = decltype(nuc)::value;
+                        const uint64_t mb = mrow >> (8 * (c0 >> 6));
+                        unsigned sp[NU];
+#pragma unroll
+                        for (int u = 0; u < NU; ++u) sp[u] = wave_incl_umax_dpp((unsigned)(mb >> (8 * u)) & 0xffu);
+#pragma unroll
+                        for (int u = 0; u < NU; ++u) {
+                            sp[u] = max(sp[u], carry);
+                            carry = (unsigned)readlane_i((int)sp[u], WAVE - 1);
+                        }
+                        // every slot loads a valid record: slots past the batch's products
+                        // read its last one and add 0 into their own slot
+                        int qc[NU];
+                        T qv[NU], qa[NU];
+                        bool val[NU];
+#pragma unroll
+                        for (int u = 0; u < NU; ++u) {
+                            const int t = gb + c0 + u * WAVE + l;
+                            val[u] = u < nu && t < Pb;
+                            const DnEnt<T> e = S.ent[(int)max(sp[u], 1u) - 1];
+                            qa[u] = e.a;
+                            const uint32_t o = e.base + (uint32_t)min(t, Pb - 1) * RB;
+                            if constexpr ((SPG_TILE_DIAG & 2) != 0) {   // timing only: no record loads
+                                qc[u] = (int)((o * 2654435761u) >> 22) & (TW - 1);
+                                qv[u] = (T)1;
+                            } else {
+                                load_rec(reinterpret_cast<const uint32_t*>(rb + o), 0, qc[u], qv[u]);
+                            }
+                        }
+#pragma unroll
+                        for (int u = 0; u < NU; ++u) {
+                            const int c = val[u] ? qc[u] : TW + l;
+                            const T pv = val[u] ? mul_rn(qa[u], qv[u]) : (T)0;
+                            if constexpr ((SPG_TILE_DIAG & 1) == 0) {   // (diag 1: no accumulation)
+                                lds_add(&S.acc[c], pv);   // chunk order = issue order
+                                S.hit[c] = 1;
+                            } else {
+                                if (pv == (T)12345) S.hit[c] = 1;
+                            }
+                        }
+                    };
+                    if (nu > 3 * U / 4) step(std::integral_constant<int, U>{});
+                    else if (nu > U / 2) step(std::integral_constant<int, 3 * U / 4>{});
+                    else step(std::integral_constant<int, U / 2>{});
+                }
+            }
+        }
+        wsync();
+        // the item's structure from hit[], 64 columns at a time
+        const int lo = g * TW;
+        int32_t* __restrict__ crow = Cj + obase;
+        T* __restrict__ xrow = Cx + obase;
+        int run = 0;
+        for (int k = 0; k < TW / WAVE; ++k) {
+            const int c = k * WAVE + l;
+            const bool h = S.hit[c] != 0;
+            const unsigned long long m = __ballot(h);
+            if (h && (SPG_TILE_DIAG & 8) == 0) {   // (diag 8, timing only: no output)
+                const int p = run + lane_rank(m);
+                crow[p] = lo + c;
+                const T v = S.acc[c];
+                xrow[p] = (alpha == (T)1) ? v : mul_rn(alpha, v);
+            }
+            run += (int)__popcll(m);
+        }
+        wsync();
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Symbolic pass over long B segments (a symbolic tile's expected segment >= SEG_MIN entries:
+// config 4's whole rows of 328 columns).  The bitmap OR is order-free, so there is no lane ->
+// product map: four A entries per instruction, one per 16-lane group, each group walking its
+// entry's B segment 16 columns (64 bytes, one cache line) at a time, 8 steps in flight.
+// Writes each numeric tile's entry count (and, for sparse numeric tiles, its bitmap), as
+// k_tile_sym.  (Measured on config 4: 4.05 ms against 7.05 ms for k_tile_sym's flattened
+// walk over 16384-column tiles and 7.0 ms for a one-entry-per-instruction cursor walk.)
+constexpr int SEG_WPB = 2;
+template <typename IP>
+__global__ __launch_bounds__(SEG_WPB * WAVE) void k_tile_sym_seg(
+    int64_t row0, int64_t nrows, int tws, int G, int twss, const IP* __restrict__ Ap,
+    const int32_t* __restrict__ Aj, const IP* __restrict__ Bp, const int32_t* __restrict__ Bj,
+    const uint32_t* __restrict__ sidx, uint32_t* __restrict__ bitmap, int64_t* __restrict__ item_cnt) {
+    constexpr int U = 8;
+    __shared__ __attribute__((aligned(16))) uint32_t bits_all[SEG_WPB][SYM_NWMAX];
+    const int l = lane_id();
+    const int sub = l & 15, grp = l >> 4;
+    const int wv = uniform((int)(threadIdx.x >> 6));
+    uint32_t* bits = bits_all[wv];
+    const int nw = (1 << tws) >> 5;
+    const int R = 1 << (twss - tws);
+    const int Gs = (G + R - 1) / R;
+    const uint32_t tasks = (uint32_t)(nrows * Gs);
+    const uint32_t stride = gridDim.x * SEG_WPB;
+    for (uint32_t task = xcd_block(gridDim.x) * SEG_WPB + wv; task < tasks; task += stride) {
+        const int64_t row = row0 + (int64_t)(task / (uint32_t)Gs);
+        const int gs = (int)(task % (uint32_t)Gs);
+        const int t0 = gs * R, t1 = min(G, t0 + R);
+        const int lo = t0 << tws;
+        const int nws = (t1 - t0) * nw;
+        const int64_t a0 = Ap[row];
+        const int nA = (int)(Ap[row + 1] - a0);
+        if (nA <= 0) {
+            for (int t = t0 + l; t < t1; t += WAVE) item_cnt[(row - row0) * G + t] = 0;
+            continue;
+        }
+        wsync();
+        for (int w = l; w < nws; w += WAVE) bits[w] = 0u;
+        wsync();
+        for (int b = 0; b < nA; b += 4) {   // entries b .. b+3, one per 16-lane group
+            int cnt = 0;
+            int64_t beg = 0;
+            if (b + grp < nA) {
+                const int32_t k = Aj[a0 + b + grp];
+                const IP rb = Bp[k];
+                if (Gs == 1) {
+                    cnt = (int)(Bp[k + 1] - rb);
+                    beg = (int64_t)rb;
+                } else {
+                    const uint32_t* sk = sidx + (int64_t)k * (Gs + 1);
+                    const uint32_t s0 = sk[gs];
+                    cnt = (int)(sk[gs + 1] - s0);
+                    beg = (int64_t)rb + s0;
+                }
+            }
+            // the longest of the four segments sets the steps (wave-uniform)
+            int mx = cnt;
+            mx = max(mx, __shfl_xor(mx, 16, WAVE));
+            mx = max(mx, __shfl_xor(mx, 32, WAVE));
+            mx = uniform(mx);
+            for (int e = 0; e < mx; e += 16 * U) {
+                int col[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int x = e + 16 * u + sub;
+                    col[u] = x < cnt ? Bj[beg + x] : -1;
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    if (col[u] >= 0) set_bit(bits, col[u] - lo);
+            }
+        }
+        wsync();
+        if (bitmap) {
+            uint32_t* __restrict__ out = bitmap + ((row - row0) * G + t0) * (int64_t)nw;
+            for (int w = l; w < nws; w += WAVE) out[w] = bits[w];
+        }
+        for (int t = l; t < t1 - t0; t += WAVE) {
+            int c = 0;
+            for (int q = 0; q < nw; ++q) c += __popc(bits[t * nw + ((q + t) & (nw - 1))]);
+            item_cnt[(row - row0) * G + t0 + t] = c;
+        }
+    }
+}
+
+}  // namespace spg

@@ -16,7 +16,9 @@ from tests.golden_cases import case_names, load
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
-ALGS = [(1, 0.2), (2, 0.2), (3, 0.2), (3, 0.05), (0, 0.2)]
+# "3c": ALG3 with its chunks kept even where the unchunked workspace is within the cap
+# (SPG_ALG3_CHUNK_ALWAYS, a schedule-only switch): the chunked paths on small inputs
+ALGS = [(1, 0.2), (2, 0.2), (3, 0.2), ("3c", 0.2), ("3c", 0.05), (0, 0.2)]
 
 
 def _dev():
@@ -24,8 +26,15 @@ def _dev():
 
 
 def _gpu(A, B, alg=2, alpha=1.0, cf=0.2):
+    import os
     from spmm_amd import cusparse
     from spmm_amd.sparse import csr_matrix
+    if alg == "3c":
+        os.environ["SPG_ALG3_CHUNK_ALWAYS"] = "1"
+        try:
+            return _gpu(A, B, 3, alpha, cf)
+        finally:
+            del os.environ["SPG_ALG3_CHUNK_ALWAYS"]
     dA = csr_matrix(A, device=_dev())
     dB = csr_matrix(B, device=_dev())
     if not (dA.has_canonical_format and dB.has_canonical_format):
@@ -83,7 +92,7 @@ def test_golden_bitexact(name, alg, cf):
     (1024, 0.01, np.float64), (2048, 0.02, np.float32), (16384, 1e-3, np.float64),
     (8192, 1e-4, np.float64), (8192, 1e-3, np.float64), (4096, 0.05, np.float64),
     (3000, 0.3, np.float32)])
-@pytest.mark.parametrize("alg", [1, 2, 3])
+@pytest.mark.parametrize("alg", [1, 2, 3, "3c"])
 def test_random_bitexact(n, density, dtype, alg):
     from spmm_amd import gen
     A, B = gen.scipy_pair(n, density, seed=n + int(density * 1e6), dtype=dtype, normal=True)
@@ -604,3 +613,30 @@ def test_product_on_non_current_device_keeps_current_device():
     torch.cuda.synchronize(1)
     _assert_same((C.indptr.cpu().numpy().astype(np.int64), C.indices.cpu().numpy(), C.data.cpu().numpy()),
                  _oracle_ref(A, A))
+
+
+def test_alg1_lb_direct_path_bitexact(tmp_path):
+    """The ALG1 numeric launch bounds every wait (its scan tiles' look-back, the rows' wait
+    for their 64-row group prefix): a wait past the bound computes the prefix directly from
+    the row counts.  SPG_LB_SPIN_TICKS=0 (read when a handle is created) sends EVERY wait down
+    that path; config 2 through it must equal the oracle bit for bit, in a fresh process."""
+    import os
+    import subprocess
+    import sys
+    out = tmp_path / "c.npz"
+    code = (
+        "import numpy as np, torch, sys\n"
+        f"sys.path.insert(0, {repr(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))})\n"
+        "from spmm_amd import cusparse, gen\n"
+        "from spmm_amd.sparse import csr_matrix\n"
+        "A, B = gen.scipy_pair(16384, 1e-3, seed=42)\n"
+        "C = cusparse.spgemm(csr_matrix(A, device='cuda:0'), csr_matrix(B, device='cuda:0'), alg=1)\n"
+        "torch.cuda.synchronize()\n"
+        f"np.savez({repr(str(out))}, p=C.indptr.cpu().numpy(), j=C.indices.cpu().numpy(), x=C.data.cpu().numpy())\n")
+    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, SPG_LB_SPIN_TICKS="0"),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    from spmm_amd import gen
+    A, B = gen.scipy_pair(16384, 1e-3, seed=42)
+    got = np.load(out)
+    _assert_same((got["p"].astype(np.int64), got["j"], got["x"]), oracle.spgemm(A, B, keep_zeros=True, sort=True))
