@@ -465,7 +465,7 @@ def run_config5(ctx, args, cfg, n, tdt, vb, hook, steps, warmup):
            "steps": steps, "warmup": warmup, "scaling": "strong", "N": n, "density": dens, "alg": alg,
            "num_products": int(P_all), "nnzC": int(nnz_all), "rows_rank0": list(rows),
            "peak_hbm_bytes_max_rank": int(peak_max), "b_broadcast_ms": None if bcast_ms is None else round(bcast_ms, 3),
-           "roofline_rank0": rf,
+           "roofline_rank0": rf, "phases_ms_per_step": {k: round(v[0] / reps, 5) for k, v in ph.items() if v[1]},
            "workload": (f"{cfg['name']}: random CSR {n}x{n} density={dens:g} {args.dtype}, ALG{alg}; "
                         f"{w} row blocks cut on the product prefix (each rank draws its own block), "
                         "B broadcast over RCCL inside every step")}

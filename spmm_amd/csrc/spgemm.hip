@@ -175,6 +175,11 @@ inline bool row_kernel_enabled() {
 #ifndef SPG_TILE_LEAN
 #define SPG_TILE_LEAN 1
 #endif
+//   SPG_SP_LEAN     0 keeps the owner-round k_tile on sparse tiles (A/B against k_tile_sp)
+#ifndef SPG_SP_LEAN
+#define SPG_SP_LEAN 1
+#endif
+
 
 struct TileVariant { int ru; bool dense; };
 inline const TileVariant& tile_variant() {
@@ -906,6 +911,14 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
                                   (const int64_t*)tile_chunk_items(p, c), cj, cx, alpha);
         };
         if constexpr (OrderedLdsAdd<T>::value) {
+            if (!dense && SPG_TILE_LEAN && SPG_SP_LEAN) {   // sparse tiles, ordered LDS adds
+                hipExtLaunchKernelGGL((k_tile_sp<T, IP>), dim3(tile_grid(n * p.G, SP_WPB)), dim3(SP_WPB * WAVE), 0,
+                                      h->stream, kt.a, kt.b, 0, r0, n, p.tws, p.G, Ap, Aj, Ax, p.B.rows,
+                                      (const uint32_t*)p.brec, (const int32_t*)p.tptr, (const uint32_t*)p.bitmap,
+                                      (const int64_t*)tile_chunk_items(p, c), cj, cx, alpha);
+                SPG_LAUNCHED(h);
+                continue;
+            }
             if (dense && SPG_TILE_LEAN) {   // ordered LDS adds (spgemm_tile_dn.hpp)
                 hipExtLaunchKernelGGL((k_tile_dn<T, IP>), dim3(tile_grid(n * p.G, DN_WPB)), dim3(DN_WPB * WAVE), 0,
                                       h->stream, kt.a, kt.b, 0, r0, n, p.tws, p.G, Ap, Aj, Ax, p.B.rows,

@@ -818,7 +818,7 @@ __device__ __forceinline__ void scan_tile(int64_t bid, int64_t n, const IN* in, 
                 __hip_atomic_store(&st[bid], (1ull << 62) | (unsigned long long)btot, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
             int64_t j = bid - 1;
-            const uint64_t t0 = wall_clock64();
+            uint64_t t0 = 0;   // (the clock is read only once a predecessor is found not ready)
             bool late = spin == 0;   // (spin 0: the direct path, for the tests)
             for (; !late;) {
                 const int64_t q = j - l;
@@ -826,9 +826,14 @@ __device__ __forceinline__ void scan_tile(int64_t bid, int64_t n, const IN* in, 
                 if (q >= 0) {
                     do {
                         s = __hip_atomic_load(&st[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        if ((s >> 62) == 0 && wall_clock64() - t0 > spin) {
-                            s = 2ull << 62;   // stop waiting (the direct sum below replaces the prefix)
-                            late = true;
+                        if ((s >> 62) == 0) {
+                            const uint64_t now = wall_clock64();
+                            if (t0 == 0) {
+                                t0 = now;
+                            } else if (now - t0 > spin) {
+                                s = 2ull << 62;   // stop waiting (the direct sum below replaces the prefix)
+                                late = true;
+                            }
                         }
                     } while ((s >> 62) == 0);
                 }

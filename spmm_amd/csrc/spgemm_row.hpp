@@ -201,9 +201,11 @@ template <typename OFF> struct RowScan {
 __device__ __forceinline__ long long row_group_prefix(const unsigned long long* gp, unsigned long long gw,
                                                       const int64_t* cnt, int64_t g0, uint64_t spin) {
     if (spin == 0) return wave_direct_sum(cnt, g0);   // (the direct path, for the tests)
-    const uint64_t t0 = wall_clock64();
+    uint64_t t0 = 0;   // (the clock is read only once the word is found not ready)
     while (!(gw & GPRE_READY)) {
-        if (wall_clock64() - t0 > spin) return wave_direct_sum(cnt, g0);
+        const uint64_t now = wall_clock64();
+        if (t0 == 0) t0 = now;
+        else if (now - t0 > spin) return wave_direct_sum(cnt, g0);
         __builtin_amdgcn_s_sleep(2);
         const unsigned long long v = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         gw = ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |

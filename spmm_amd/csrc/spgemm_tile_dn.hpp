@@ -45,22 +45,212 @@ template <typename T> struct __attribute__((aligned(16))) DnEnt {
     T a;
 };
 
-template <typename T> struct DnLds {
+// fp64 items take their structure from the accumulator itself (SPG_DN_SENT): every slot
+// starts at -0.0 instead of +0.0.  -0.0 + p == +0.0 + p for every p except p == -0.0, so a
+// column's sum equals scipy's (which starts at +0.0) except while every product it has seen
+// is -0.0 (ours -0.0, scipy's +0.0).  So a column is reached iff its slot is not -0.0 or it
+// saw only -0.0 products; the item's symbolic count tells which case holds: fewer non -0.0
+// slots than entries sends the item down a rare path that re-walks its products and turns
+// each reached -0.0 slot into scipy's +0.0.  No hit byte per product.
+#ifndef SPG_DN_SENT
+#define SPG_DN_SENT 1
+#endif
+template <typename T> constexpr bool dn_sent() { return SPG_DN_SENT && std::is_same<T, double>::value; }
+
+template <typename T, bool HIT = !dn_sent<T>()> struct DnLds {
     T acc[DN_TW + WAVE];          // accumulator by column; + one lane-private slot per lane
     DnEnt<T> ent[WAVE];
-    uint8_t hit[DN_TW + WAVE];    // columns some product reached (the item's structure)
     uint8_t mk[NUM_MK];           // lane -> A-entry markers of 8 chunks
+    uint8_t hit[DN_TW + WAVE];    // columns some product reached (non-sentinel types)
+};
+// (dn_sent: 10,240 bytes per wave -- 8 two-wave blocks, 16 waves, fit a CU's 160 KB)
+template <typename T> struct DnLds<T, false> {
+    T acc[DN_TW + WAVE];
+    DnEnt<T> ent[WAVE];
+    uint8_t mk[NUM_MK];
 };
 
-// Numeric pass on dense tiles (TW <= 1024 columns): one wave per (row, tile) item, items
-// tile-major over the XCD-aware block map (as k_tile).  Per batch of 64 A entries: each lane's
-// entry, value and tile segment (the first NB batches preloaded); a DPP scan of the segment
-// lengths; the entry table in LDS.  Per group of 8 chunks the transposed markers; per U
-// chunks: the lane -> entry max-scans, one table read and one record load per chunk (all in
-// flight), then per chunk in order one multiply, one ds_add_f64 into acc[column] and one byte
-// store into hit[column].  Lanes past the batch's products add 0 into their own private
-// slot.  The item's output: 64 columns at a time from hit[] (ballot + lane rank give
-// positions), straight to C at its offset.
+constexpr uint64_t NEG_ZERO = 0x8000000000000000ull;
+
+// The ordered product walk of one item (row, tile): its A entries in batches of 64 (the first
+// NB batches' tile segments `sq` and values `aq` given, the rest loaded here); per batch a DPP
+// scan of the segment lengths and the entry table in LDS; per group of 8 chunks the transposed
+// markers; per U chunks the lane -> entry max-scans, one 16-byte table read and one record load
+// per chunk (all in flight), then per chunk in order one multiply and one ds_add_f64 into
+// acc[slot(valid, column)] -- slot() maps a product's tile column to its accumulator slot, or
+// to DUMMY + lane (a lane-private slot: the lane adds 0) -- and hit(slot).
+template <typename T, int NB, int DUMMY, typename L, typename Slot, typename Hit>
+__device__ __forceinline__ void dn_walk(L* lp, T* acc, int l, int TWD, const int32_t* __restrict__ tp,
+                                        int64_t a0, int nA, const T (&aq)[NB], const uint2 (&sq)[NB],
+                                        const int32_t* __restrict__ Aj, const T* __restrict__ Ax,
+                                        const char* __restrict__ rb, Slot&& slot, Hit&& hit) {
+    constexpr int U = sizeof(T) > 8 ? 4 : 8;     // chunks in flight
+    constexpr uint32_t RB = 4u * (uint32_t)rec_words<T>();   // bytes of one B record
+    DnEnt<T>* ent = lp->ent;
+    uint8_t* mk = lp->mk;
+    for (int b = 0; b < nA; b += WAVE) {
+        int cnt = 0;
+        uint32_t beg = 0;
+        T av = (T)0;
+        if (b < NB * WAVE) {
+#pragma unroll
+            for (int q = 0; q < NB; ++q)
+                if (q == (b >> 6)) {
+                    cnt = (int)(sq[q].y - sq[q].x);
+                    beg = sq[q].x;
+                    av = aq[q];
+                }
+        } else if (b + l < nA) {
+            const uint2 se = seg_pair(tp, Aj[a0 + b + l]);
+            cnt = (int)(se.y - se.x);
+            beg = se.x;
+            av = Ax[a0 + b + l];
+        }
+        const int incl = wave_incl_sum_dpp(cnt);
+        const int off = incl - cnt;
+        const int Pb = readlane_i(incl, WAVE - 1);
+        wsync();
+        ent[l].base = beg * RB - (uint32_t)off * RB;   // wraps; base + t*RB is exact
+        ent[l].a = av;
+        unsigned carry = 0u;
+        for (int gb = 0; gb < Pb; gb += NUM_MK) {
+            num_group_markers(*lp, l, cnt, off, gb);
+            const int nchg = min(NUM_MK, Pb - gb);
+            const uint2 m2 = reinterpret_cast<const uint2*>(mk)[l];
+            const uint64_t mrow = ((uint64_t)m2.y << 32) | m2.x;
+            for (int c0 = 0; c0 < nchg; c0 += U * WAVE) {
+                const int nu = min(U, (nchg - c0 + WAVE - 1) >> 6);
+                auto step = [&](auto nuc) {
+                    constexpr int NU = decltype(nuc)::value;
+                    const uint64_t mb = mrow >> (8 * (c0 >> 6));
+                    unsigned sp[NU];
+#pragma unroll
+                    for (int u = 0; u < NU; ++u) sp[u] = wave_incl_umax_dpp((unsigned)(mb >> (8 * u)) & 0xffu);
+#pragma unroll
+                    for (int u = 0; u < NU; ++u) {
+                        sp[u] = max(sp[u], carry);
+                        carry = (unsigned)readlane_i((int)sp[u], WAVE - 1);
+                    }
+                    // every slot loads a valid record: slots past the batch's products read
+                    // its last one and add 0 into their own slot
+                    int qc[NU];
+                    T qv[NU], qa[NU];
+                    bool val[NU];
+#pragma unroll
+                    for (int u = 0; u < NU; ++u) {
+                        const int t = gb + c0 + u * WAVE + l;
+                        val[u] = u < nu && t < Pb;
+                        uint32_t eb;
+                        if constexpr (sizeof(T) == 8) {   // base and value with one 16-byte read
+                            const uint4 e4 = reinterpret_cast<const uint4*>(ent)[(int)max(sp[u], 1u) - 1];
+                            eb = e4.x;
+                            qa[u] = __hiloint2double((int)e4.w, (int)e4.z);
+                        } else {
+                            const DnEnt<T> e = ent[(int)max(sp[u], 1u) - 1];
+                            eb = e.base;
+                            qa[u] = e.a;
+                        }
+                        const uint32_t o = eb + __umul24((uint32_t)min(t, Pb - 1), RB);
+                        if constexpr ((SPG_TILE_DIAG & 2) != 0) {   // timing only: no record loads
+                            qc[u] = (int)((o * 2654435761u) >> 22) & (TWD - 1);
+                            qv[u] = (T)1;
+                        } else {
+                            load_rec(reinterpret_cast<const uint32_t*>(rb + o), 0, qc[u], qv[u]);
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < NU; ++u) {
+                        const int c = slot(val[u], qc[u]);
+                        const T pv = c < DUMMY ? mul_rn(qa[u], qv[u]) : (T)0;
+                        if constexpr ((SPG_TILE_DIAG & 1) == 0) {   // (diag 1: no accumulation)
+                            lds_add(&acc[c], pv);   // chunk order = issue order
+                            hit(c);
+                        } else {
+                            if (pv == (T)12345) hit(c);
+                        }
+                    }
+                };
+                if (nu > 3 * U / 4) step(std::integral_constant<int, U>{});
+                else if (nu > U / 2) step(std::integral_constant<int, 3 * U / 4>{});
+                else step(std::integral_constant<int, U / 2>{});
+            }
+        }
+    }
+}
+
+// One dense-tile item (row, tile g of TW <= 1024 columns) on one wave: clear the accumulator,
+// the ordered product walk with slot = column, then the output 64 columns at a time from hit[]
+// or (dn_sent) the slots that left -0.0 (ballot + lane rank give positions), straight to C.
+template <typename T, int NB>
+__device__ __forceinline__ void dn_item(DnLds<T>& S, int l, int TW, int lo, int nnz, const int32_t* __restrict__ tp,
+                                        int64_t a0, int nA, const T (&aq)[NB], const uint2 (&sq)[NB],
+                                        const int32_t* __restrict__ Aj, const T* __restrict__ Ax,
+                                        const char* __restrict__ rb, int32_t* __restrict__ crow,
+                                        T* __restrict__ xrow, T alpha) {
+    constexpr uint32_t RB = 4u * (uint32_t)rec_words<T>();
+    wsync();
+    {   // clear the accumulator (-0.0: dn_sent) and the hit bytes (16-byte stores; TW is a
+        // multiple of 64)
+        uint4* a4 = reinterpret_cast<uint4*>(S.acc);
+        const uint32_t hi = dn_sent<T>() ? 0x80000000u : 0u;
+        for (int q = l; q < TW * (int)sizeof(T) / 16; q += WAVE) a4[q] = make_uint4(0u, hi, 0u, hi);
+        if constexpr (!dn_sent<T>()) {
+            uint4* h4 = reinterpret_cast<uint4*>(S.hit);
+            for (int q = l; q < TW / 16; q += WAVE) h4[q] = make_uint4(0u, 0u, 0u, 0u);
+        }
+    }
+    dn_walk<T, NB, DN_TW>(&S, S.acc, l, TW, tp, a0, nA, aq, sq, Aj, Ax, rb,
+                          [&](bool valid, int c) { return valid ? c : DN_TW + l; },
+                          [&](int c) {
+                              if constexpr (!dn_sent<T>()) S.hit[c] = 1;
+                          });
+    wsync();
+    // the item's structure, 64 columns at a time: hit[] or (dn_sent) the non -0.0 slots
+    auto emit = [&]() {
+        int run = 0;
+        for (int k = 0; k < TW / WAVE; ++k) {
+            const int c = k * WAVE + l;
+            const T v = S.acc[c];
+            bool h;
+            if constexpr (dn_sent<T>()) h = __double_as_longlong(v) != (long long)NEG_ZERO;
+            else h = S.hit[c] != 0;
+            const unsigned long long m = __ballot(h);
+            if (h && (SPG_TILE_DIAG & 8) == 0) {   // (diag 8, timing only: no output)
+                const int p = run + lane_rank(m);
+                crow[p] = lo + c;
+                xrow[p] = (alpha == (T)1) ? v : mul_rn(alpha, v);
+            }
+            run += (int)__popcll(m);
+        }
+        return run;
+    };
+    const int got = emit();
+    if constexpr (dn_sent<T>()) {
+        if (got < nnz && (SPG_TILE_DIAG & 9) == 0) {
+            // rare: a reached column saw only -0.0 products -- its slot is still -0.0, scipy's
+            // sum is +0.0.  Re-walk the item's records (one lane per A entry) and turn every
+            // reached -0.0 slot into +0.0, then write the item again.
+            for (int b = 0; b < nA; b += WAVE) {
+                if (b + l < nA) {
+                    const uint2 se = seg_pair(tp, Aj[a0 + b + l]);
+                    for (uint32_t i = se.x; i < se.y; ++i) {
+                        int c;
+                        T v;
+                        load_rec(reinterpret_cast<const uint32_t*>(rb + (uint64_t)i * RB), 0, c, v);
+                        if (__double_as_longlong(S.acc[c]) == (long long)NEG_ZERO) S.acc[c] = 0.0;
+                    }
+                }
+            }
+            wsync();
+            emit();
+        }
+    }
+}
+
+// Numeric pass on dense tiles: one wave per (row, tile) item, items tile-major over the
+// XCD-aware block map (an XCD works through one tile at a time, so the tile's B slice and
+// segment table stay in its L2), the first NB batches' A entries and tile segments loaded up
+// front.
 template <typename T, typename IP>
 __global__ __launch_bounds__(DN_WPB * WAVE) void k_tile_dn(
     int64_t row0, int64_t nrows, int tws, int G, const IP* __restrict__ Ap,
@@ -68,9 +258,7 @@ __global__ __launch_bounds__(DN_WPB * WAVE) void k_tile_dn(
     const uint32_t* __restrict__ brec, const int32_t* __restrict__ tptr,
     const int64_t* __restrict__ item_off, int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha) {
     static_assert(OrderedLdsAdd<T>::value, "ordered LDS add needed");
-    constexpr int U = sizeof(T) > 8 ? 4 : 8;     // chunks in flight
     constexpr int NB = sizeof(T) > 8 ? 4 : 8;    // A batches preloaded per item
-    constexpr uint32_t RB = 4u * (uint32_t)rec_words<T>();   // bytes of one B record
     __shared__ __attribute__((aligned(16))) DnLds<T> lds[DN_WPB];
     const int l = lane_id();
     const int wv = uniform((int)(threadIdx.x >> 6));
@@ -88,7 +276,6 @@ __global__ __launch_bounds__(DN_WPB * WAVE) void k_tile_dn(
         const int32_t* __restrict__ tp = tptr + (int64_t)g * (K + 1);
         const int64_t a0 = Ap[row];
         const int nA = (int)(Ap[row + 1] - a0);
-        // the first NB batches' A entries, values and tile segments, loaded up front
         int32_t kq[NB];
         T aq[NB];
         uint2 sq[NB];
@@ -102,116 +289,130 @@ __global__ __launch_bounds__(DN_WPB * WAVE) void k_tile_dn(
             }
         }
 #pragma unroll
-        for (int q = 0; q < NB; ++q) {
-            sq[q] = make_uint2(0u, 0u);
-            if (kq[q] >= 0) sq[q] = seg_pair(tp, kq[q]);
-        }
-        wsync();
-        {   // clear the accumulator and the hit bytes (16-byte stores; TW is a multiple of 64)
-            uint4* a4 = reinterpret_cast<uint4*>(S.acc);
-            for (int q = l; q < TW * (int)sizeof(T) / 16; q += WAVE) a4[q] = make_uint4(0u, 0u, 0u, 0u);
-            uint4* h4 = reinterpret_cast<uint4*>(S.hit);
-            for (int q = l; q < TW / 16; q += WAVE) h4[q] = make_uint4(0u, 0u, 0u, 0u);
-        }
-        for (int b = 0; b < nA; b += WAVE) {
-            int cnt = 0;
-            uint32_t beg = 0;
-            T av = (T)0;
-            if (b < NB * WAVE) {
+        for (int q = 0; q < NB; ++q) sq[q] = kq[q] >= 0 ? seg_pair(tp, kq[q]) : make_uint2(0u, 0u);
+        dn_item<T, NB>(S, l, TW, g * TW, nnz, tp, a0, nA, aq, sq, Aj, Ax, rb, Cj + obase, Cx + obase, alpha);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Numeric pass on sparse tiles (TW up to 4096 columns, config 5's shape): the item's structure
+// is its symbolic bitmap; the accumulator is compact -- a product's slot is its column's rank
+// among the item's columns (the bitmap word's popcount prefix plus the bits below it) -- in
+// windows of at most TILE_CAP slots (an item with more entries re-walks its products once
+// per window).  The same ordered walk as the dense tiles (one ds_add_f64 per 64 products);
+// the output, 64 columns at a time from the bitmap, straight to C.
+template <typename T> struct SpLds {
+    T acc[TILE_CAP + WAVE];       // compact accumulator of one window; + lane-private slots
+    uint2 bw[TILE_NWMAX];         // (bitmap word, popcount prefix)
+    DnEnt<T> ent[WAVE];
+    uint8_t mk[NUM_MK];
+};
+constexpr int SP_WPB = 1;   // 11.3 KB of LDS per wave: one-wave blocks pack a CU best
+
+template <typename T, typename IP>
+__global__ __launch_bounds__(SP_WPB * WAVE) void k_tile_sp(
+    int64_t row0, int64_t nrows, int tws, int G, const IP* __restrict__ Ap,
+    const int32_t* __restrict__ Aj, const T* __restrict__ Ax, int64_t K,
+    const uint32_t* __restrict__ brec, const int32_t* __restrict__ tptr, const uint32_t* __restrict__ bitmap,
+    const int64_t* __restrict__ item_off, int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha) {
+    static_assert(OrderedLdsAdd<T>::value, "ordered LDS add needed");
+    constexpr int NB = sizeof(T) > 8 ? 4 : 8;
+    __shared__ __attribute__((aligned(16))) SpLds<T> lds[SP_WPB];
+    const int l = lane_id();
+    const int wv = uniform((int)(threadIdx.x >> 6));
+    SpLds<T>& S = lds[wv];
+    const int TW = 1 << tws;
+    const int nw = TW >> 5;                    // bitmap words of a tile
+    const int wpl = (nw + WAVE - 1) / WAVE;    // words per lane (<= 2)
+    const char* __restrict__ rb = reinterpret_cast<const char*>(brec);
+    const uint32_t items = (uint32_t)(nrows * G);
+    for (uint32_t it = xcd_block(gridDim.x) * SP_WPB + wv; it < items; it += gridDim.x * SP_WPB) {
+        const int g = (int)(it / (uint32_t)nrows);
+        const int64_t row = row0 + (int64_t)(it - (uint32_t)g * (uint32_t)nrows);
+        const int64_t item = (row - row0) * G + g;
+        const int32_t* __restrict__ tp = tptr + (int64_t)g * (K + 1);
+        const int64_t a0 = Ap[row];
+        const int nA = (int)(Ap[row + 1] - a0);
+        if (nA <= 0) continue;
+        // the item's bitmap (lane owns wpl words) and its popcount prefix
+        const uint32_t* __restrict__ ibits = bitmap + item * nw;
+        const int w0 = min(nw, l * wpl), w1 = min(nw, w0 + wpl);
+        uint32_t wd[2] = {0u, 0u};
+        int mine = 0;
 #pragma unroll
-                for (int q = 0; q < NB; ++q)
-                    if (q == (b >> 6)) {
-                        cnt = (int)(sq[q].y - sq[q].x);
-                        beg = sq[q].x;
-                        av = aq[q];
-                    }
-            } else if (b + l < nA) {
-                const uint2 se = seg_pair(tp, Aj[a0 + b + l]);
-                cnt = (int)(se.y - se.x);
-                beg = se.x;
-                av = Ax[a0 + b + l];
+        for (int q = 0; q < 2; ++q)
+            if (w0 + q < w1) {
+                wd[q] = ibits[w0 + q];
+                mine += __popc(wd[q]);
             }
-            const int incl = wave_incl_sum_dpp(cnt);
-            const int off = incl - cnt;
-            const int Pb = readlane_i(incl, WAVE - 1);
+        const int pincl = wave_incl_sum_dpp(mine);
+        const int nnz = readlane_i(pincl, WAVE - 1);
+        if (nnz == 0) continue;
+        const int p0 = pincl - mine;
+        int32_t kq[NB];
+        T aq[NB];
+        uint2 sq[NB];
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+            kq[q] = -1;
+            aq[q] = (T)0;
+            if (q * WAVE + l < nA) {
+                kq[q] = Aj[a0 + q * WAVE + l];
+                aq[q] = Ax[a0 + q * WAVE + l];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < NB; ++q) sq[q] = kq[q] >= 0 ? seg_pair(tp, kq[q]) : make_uint2(0u, 0u);
+        const int64_t obase = item_off[item];
+        wsync();
+        {
+            int run = p0;
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+                if (w0 + q < w1) {
+                    S.bw[w0 + q] = make_uint2(wd[q], (uint32_t)run);
+                    run += __popc(wd[q]);
+                }
+        }
+        const int lo = g * TW;
+        for (int L0 = 0; L0 < WAVE;) {
+            // window: lanes [L0, L1) whose words' entries fit TILE_CAP slots
+            int L1 = WAVE, wb = 0, wn = nnz;
+            if (nnz > TILE_CAP) {
+                wb = readlane_i(p0, L0);
+                L1 = (int)__popcll(__ballot(pincl <= wb + TILE_CAP));
+                if (L1 <= L0) L1 = L0 + 1;
+                wn = (L1 < WAVE ? readlane_i(p0, L1) : nnz) - wb;
+            }
+            const int clo = 32 * wpl * L0, chi = 32 * wpl * L1;   // window, tile-relative
             wsync();
-            S.ent[l].base = beg * RB - (uint32_t)off * RB;   // wraps; base + t*RB is exact
-            S.ent[l].a = av;
-            unsigned carry = 0u;
-            for (int gb = 0; gb < Pb; gb += NUM_MK) {
-                num_group_markers(S, l, cnt, off, gb);
-                const int nchg = min(NUM_MK, Pb - gb);
-                const uint2 m2 = reinterpret_cast<const uint2*>(S.mk)[l];
-                const uint64_t mrow = ((uint64_t)m2.y << 32) | m2.x;
-                for (int c0 = 0; c0 < nchg; c0 += U * WAVE) {
-                    const int nu = min(U, (nchg - c0 + WAVE - 1) >> 6);
-                    auto step = [&](auto nuc) {
-                        constexpr int NU = decltype(nuc)::value;
-                        const uint64_t mb = mrow >> (8 * (c0 >> 6));
-                        unsigned sp[NU];
-#pragma unroll
-                        for (int u = 0; u < NU; ++u) sp[u] = wave_incl_umax_dpp((unsigned)(mb >> (8 * u)) & 0xffu);
-#pragma unroll
-                        for (int u = 0; u < NU; ++u) {
-                            sp[u] = max(sp[u], carry);
-                            carry = (unsigned)readlane_i((int)sp[u], WAVE - 1);
-                        }
-                        // every slot loads a valid record: slots past the batch's products
-                        // read its last one and add 0 into their own slot
-                        int qc[NU];
-                        T qv[NU], qa[NU];
-                        bool val[NU];
-#pragma unroll
-                        for (int u = 0; u < NU; ++u) {
-                            const int t = gb + c0 + u * WAVE + l;
-                            val[u] = u < nu && t < Pb;
-                            const DnEnt<T> e = S.ent[(int)max(sp[u], 1u) - 1];
-                            qa[u] = e.a;
-                            const uint32_t o = e.base + (uint32_t)min(t, Pb - 1) * RB;
-                            if constexpr ((SPG_TILE_DIAG & 2) != 0) {   // timing only: no record loads
-                                qc[u] = (int)((o * 2654435761u) >> 22) & (TW - 1);
-                                qv[u] = (T)1;
-                            } else {
-                                load_rec(reinterpret_cast<const uint32_t*>(rb + o), 0, qc[u], qv[u]);
-                            }
-                        }
-#pragma unroll
-                        for (int u = 0; u < NU; ++u) {
-                            const int c = val[u] ? qc[u] : TW + l;
-                            const T pv = val[u] ? mul_rn(qa[u], qv[u]) : (T)0;
-                            if constexpr ((SPG_TILE_DIAG & 1) == 0) {   // (diag 1: no accumulation)
-                                lds_add(&S.acc[c], pv);   // chunk order = issue order
-                                S.hit[c] = 1;
-                            } else {
-                                if (pv == (T)12345) S.hit[c] = 1;
-                            }
-                        }
-                    };
-                    if (nu > 3 * U / 4) step(std::integral_constant<int, U>{});
-                    else if (nu > U / 2) step(std::integral_constant<int, 3 * U / 4>{});
-                    else step(std::integral_constant<int, U / 2>{});
+            for (int p = l; p < wn; p += WAVE) S.acc[p] = (T)0;
+            dn_walk<T, NB, TILE_CAP>(&S, S.acc, l, TW, tp, a0, nA, aq, sq, Aj, Ax, rb,
+                                     [&](bool valid, int rc) -> int {
+                                         if (!valid || rc < clo || rc >= chi) return TILE_CAP + l;
+                                         const uint2 b = S.bw[rc >> 5];
+                                         return (int)b.y + __popc(b.x & ((1u << (rc & 31)) - 1u)) - wb;
+                                     },
+                                     [&](int) {});
+            wsync();
+            // the window's entries, 64 columns (one lane's wpl words) at a time
+            for (int k = L0; k < L1; ++k) {
+                const int c = 32 * wpl * k + l;   // tile-relative column of this lane
+                bool h = false;
+                int pre = 0;
+                if (c < TW) {
+                    const uint2 b = S.bw[c >> 5];
+                    h = (b.x >> (c & 31)) & 1u;
+                    pre = (int)b.y + __popc(b.x & ((1u << (c & 31)) - 1u));
+                }
+                if (h && (SPG_TILE_DIAG & 8) == 0) {
+                    Cj[obase + pre] = lo + c;
+                    const T v = S.acc[pre - wb];
+                    Cx[obase + pre] = (alpha == (T)1) ? v : mul_rn(alpha, v);
                 }
             }
+            L0 = L1;
         }
-        wsync();
-        // the item's structure from hit[], 64 columns at a time
-        const int lo = g * TW;
-        int32_t* __restrict__ crow = Cj + obase;
-        T* __restrict__ xrow = Cx + obase;
-        int run = 0;
-        for (int k = 0; k < TW / WAVE; ++k) {
-            const int c = k * WAVE + l;
-            const bool h = S.hit[c] != 0;
-            const unsigned long long m = __ballot(h);
-            if (h && (SPG_TILE_DIAG & 8) == 0) {   // (diag 8, timing only: no output)
-                const int p = run + lane_rank(m);
-                crow[p] = lo + c;
-                const T v = S.acc[c];
-                xrow[p] = (alpha == (T)1) ? v : mul_rn(alpha, v);
-            }
-            run += (int)__popcll(m);
-        }
-        wsync();
     }
 }
 
