@@ -237,7 +237,10 @@ inline unsigned tile_grid(int64_t tasks, int wpb = TILE_WPB) {
 // and at the (pow2-rounded) row width.  When the widest symbolic tile (65536 columns or the
 // whole row) holds segments of >= SEG_MIN entries, that width and the segment-walking
 // symbolic kernel (k_tile_sym_seg) are used instead.
-constexpr double SEG_MIN = 160.0;
+#ifndef SPG_SEG_MIN
+#define SPG_SEG_MIN 128
+#endif
+constexpr double SEG_MIN = SPG_SEG_MIN;   // (config 5 segments of 65: 25.9 ms against 20.7 for k_tile_sym)
 inline int sym_tile_log2(const spg_csr_t& B, int tws, bool* seg = nullptr) {
     const double avgB = B.rows > 0 ? (double)B.nnz / (double)B.rows : 0.0;
     int tmax = tws;

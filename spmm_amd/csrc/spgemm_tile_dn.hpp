@@ -417,7 +417,7 @@ __global__ __launch_bounds__(SP_WPB * WAVE) void k_tile_sp(
 }
 
 // ---------------------------------------------------------------------------------------
-// Symbolic pass over long B segments (a symbolic tile's expected segment >= SEG_MIN entries:
+// Symbolic pass over long B segments (a symbolic tile's expected segment >= SEG_MIN = 128 entries:
 // config 4's whole rows of 328 columns).  The bitmap OR is order-free, so there is no lane ->
 // product map: four A entries per instruction, one per 16-lane group, each group walking its
 // entry's B segment 16 columns (64 bytes, one cache line) at a time, 8 steps in flight.
