@@ -113,16 +113,31 @@ def _free_port():
     return port
 
 
+def _forward(pipe, rank):
+    """A worker's stdout: rank 0's JSON line to our stdout, everything else (the collective
+    libraries' banners) to stderr, so the parent prints exactly ONE JSON line."""
+    for raw in iter(pipe.readline, b""):
+        line = raw.decode(errors="replace")
+        out = sys.stdout if rank == 0 and line.lstrip().startswith("{") else sys.stderr
+        out.write(line)
+        out.flush()
+    pipe.close()
+
+
 def spawn_workers(n, argv):
     """`--gpus N` without a launcher: start N fresh worker processes of this script (rank r
     on GPU r), wait for all of them and return the worst exit status.  Runs before anything
-    touches the GPU and never re-execs this process.  Rank 0 prints the JSON line."""
+    touches the GPU and never re-execs this process.  Rank 0's JSON line is the output."""
+    import threading
     port = _free_port()
-    procs = []
+    procs, readers = [], []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=subprocess.PIPE))
+        readers.append(threading.Thread(target=_forward, args=(procs[-1].stdout, r), daemon=True))
+        readers[-1].start()
     rcs = [None] * n
     while any(rc is None for rc in rcs):
         for i, p in enumerate(procs):
@@ -141,6 +156,8 @@ def spawn_workers(n, argv):
                         rcs[i] = p.wait()
             break
         time.sleep(0.05)
+    for t in readers:
+        t.join(timeout=30)
     bad = [rc for rc in rcs if rc != 0]
     return bad[0] if bad else 0
 
@@ -317,6 +334,17 @@ def load_hook(spec):
     return getattr(importlib.import_module(mod), fn)
 
 
+def tile_kernel(ctx, A, B, alg, cf):
+    """Name of the numeric tile kernel the product runs (dense or sparse tiles)."""
+    if not ctx.gpu or B is None:
+        return "k_tile"
+    from spmm_amd import cusparse
+    info = cusparse.plan_info(A, B, alg=alg, chunk_fraction=cf)
+    if info["path"] != "tile":
+        return info["path"]
+    return ("k_tile_dn" if info["dense_tiles"] else "k_tile_sp") + f" (TW={info['tile_width']}, {len(info['chunk_rows']) - 1} chunk(s))"
+
+
 def gen_device(ctx, n, dens, seed, tdt, rows=None, row_offset=0):
     from spmm_amd import gen
     return gen.random_csr(n if rows is None else rows, n, dens, seed=seed, dtype=tdt, device=ctx.dev,
@@ -367,8 +395,8 @@ def run_config4(ctx, args, cfg, tdt, vb, hook):
     bid, sid = lib_ids(ctx)
     key = f"c4_n{n}_d{dens:g}_{args.dtype}_alg{alg}_w1"   # per-rank work = the N=1 product
     traffic, tb = traffic_for(args.pmc, key, bid, sid) if ctx.gpu else (None, None)
-    rf = roofline(ph, reps, "k_tile", compulsory_bytes(A.shape[0], n, A.nnz, nnzB, nnzC, vb, ib_c),
-                  ms, traffic, tb, step_frac=(w == 1))
+    rf = roofline(ph, reps, tile_kernel(ctx, A, B, alg, cf),
+                  compulsory_bytes(A.shape[0], n, A.nnz, nnzB, nnzC, vb, ib_c), ms, traffic, tb, step_frac=(w == 1))
     cpu = None
     if r == 0 and w == 1 and args.cpu_seconds > 0 and ctx.gpu:
         A_h, B_h = A.get(), B.get()
@@ -459,7 +487,7 @@ def run_config5(ctx, args, cfg, n, tdt, vb, hook, steps, warmup):
     ms = elapsed / steps * 1e3
     reps = 1
     ph = phase_times(ctx, step, reps)
-    rf = roofline(ph, reps, "k_tile", compulsory_bytes(A.shape[0], n, A.nnz, nnzB, nnzC, vb, ib_c),
+    rf = roofline(ph, reps, tile_kernel(ctx, A, B, alg, cf), compulsory_bytes(A.shape[0], n, A.nnz, nnzB, nnzC, vb, ib_c),
                   ms, None, None, step_frac=False)
     out = {"gflops": round(2.0 * P_all * steps / elapsed / 1e9, 3), "ms_per_step": round(ms, 5),
            "steps": steps, "warmup": warmup, "scaling": "strong", "N": n, "density": dens, "alg": alg,
