@@ -68,6 +68,42 @@ __global__ __launch_bounds__(64) void k_round(int n, const double* __restrict__ 
     }
 }
 
+// Q4/Q5: the same two questions for ds_add_f32 (LDS atomic float add).
+__global__ __launch_bounds__(64) void k_round32(int n, const float* __restrict__ x, const float* __restrict__ y,
+                                                float* __restrict__ lds_sum, float* __restrict__ valu_sum) {
+    __shared__ float s[64];
+    const int l = threadIdx.x;
+    for (int i = blockIdx.x * 64 + l; i < n; i += gridDim.x * 64) {
+        s[l] = x[i];
+        __hip_atomic_fetch_add(&s[l], y[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        lds_sum[i] = s[l];
+        valu_sum[i] = __fadd_rn(x[i], y[i]);
+    }
+}
+__global__ __launch_bounds__(64) void k_order32(int trials, const float* __restrict__ init, const float* __restrict__ v,
+                                                const int* __restrict__ a, const unsigned long long* __restrict__ act,
+                                                float* __restrict__ out) {
+    __shared__ float s[SLOTS];
+    const int l = threadIdx.x;
+    for (int t = blockIdx.x; t < trials; t += gridDim.x) {
+        for (int i = l; i < SLOTS; i += 64) s[i] = init[(size_t)t * SLOTS + i];
+        __syncthreads();
+        if ((act[t] >> l) & 1ull)
+            __hip_atomic_fetch_add(&s[a[(size_t)t * 64 + l]], v[(size_t)t * 64 + l], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __syncthreads();
+        for (int i = l; i < SLOTS; i += 64) out[(size_t)t * SLOTS + i] = s[i];
+        __syncthreads();
+    }
+}
+
+static bool same_bits32(float a, float b) {
+    if (std::isnan(a) && std::isnan(b)) return true;
+    uint32_t x, y;
+    std::memcpy(&x, &a, 4);
+    std::memcpy(&y, &b, 4);
+    return x == y;
+}
+
 static bool same_bits(double a, double b) {
     if (std::isnan(a) && std::isnan(b)) return true;
     uint64_t x, y;
@@ -173,6 +209,64 @@ int main(int argc, char** argv) {
         std::printf("Q%d %s: %d trials, %ld same-address lane pairs; mismatches vs ascending-lane order %ld, "
                     "vs descending %ld%s\n", rtn ? 3 : 2, rtn ? "ds_add_rtn_f64" : "ds_add_f64", trials, conflicts,
                     bad, badrev, rtn ? (badret ? " (returned old values out of order)" : " (returned old values in lane order)") : "");
+    }
+    // ---- Q4 (f32 rounding incl. denormals) and Q5 (f32 lane order)
+    {
+        std::vector<float> xf(n1), yf(n1), lf(n1), vf(n1);
+        for (int i = 0; i < n1; ++i) {
+            const int mode = (i >> 18) & 3;
+            auto rv = [&](int m) -> float {
+                std::uniform_real_distribution<float> u(1.0f, 2.0f);
+                const float mm = u(g) * ((g() & 1) ? -1.f : 1.f);
+                if (m == 0) return std::ldexp(mm, std::uniform_int_distribution<int>(-30, 30)(g));
+                if (m == 1) return std::ldexp(mm, std::uniform_int_distribution<int>(-149, -120)(g));   // denormals
+                if (m == 2) return std::ldexp(mm, std::uniform_int_distribution<int>(-3, 3)(g));
+                const float sp[] = {INFINITY, -INFINITY, NAN, 0.0f, -0.0f, 1.4e-45f, -1.4e-45f, 3.4028235e38f};
+                return sp[std::uniform_int_distribution<int>(0, 7)(g)];
+            };
+            xf[i] = rv(mode);
+            yf[i] = rv((mode + (i & 1)) & 3);
+        }
+        float *dxf, *dyf, *dlf, *dvf;
+        CK(hipMalloc(&dxf, 4 * n1)); CK(hipMalloc(&dyf, 4 * n1)); CK(hipMalloc(&dlf, 4 * n1)); CK(hipMalloc(&dvf, 4 * n1));
+        CK(hipMemcpy(dxf, xf.data(), 4 * n1, hipMemcpyHostToDevice));
+        CK(hipMemcpy(dyf, yf.data(), 4 * n1, hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(k_round32, dim3(4096), dim3(64), 0, 0, n1, dxf, dyf, dlf, dvf);
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(lf.data(), dlf, 4 * n1, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(vf.data(), dvf, 4 * n1, hipMemcpyDeviceToHost));
+        long b4 = 0, b4h = 0;
+        for (int i = 0; i < n1; ++i) {
+            if (!same_bits32(lf[i], vf[i])) { if (b4 < 5) std::printf("Q4 mismatch x=%a y=%a lds=%a valu=%a\n", xf[i], yf[i], lf[i], vf[i]); ++b4; }
+            if (!same_bits32(vf[i], xf[i] + yf[i])) ++b4h;
+        }
+        std::printf("Q4 ds_add_f32 vs v_add_f32: %d cases, %ld mismatches (v_add_f32 vs host: %ld)\n", n1, b4, b4h);
+        std::vector<float> initf((size_t)trials * SLOTS), vv((size_t)trials * 64), outf((size_t)trials * SLOTS);
+        for (size_t i = 0; i < initf.size(); ++i) initf[i] = (float)init[i];
+        for (size_t i = 0; i < vv.size(); ++i) vv[i] = (float)v[i];
+        float *di2, *dv3, *do2;
+        CK(hipMalloc(&di2, 4 * initf.size())); CK(hipMalloc(&dv3, 4 * vv.size())); CK(hipMalloc(&do2, 4 * outf.size()));
+        CK(hipMemcpy(di2, initf.data(), 4 * initf.size(), hipMemcpyHostToDevice));
+        CK(hipMemcpy(dv3, vv.data(), 4 * vv.size(), hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(k_order32, dim3(2048), dim3(64), 0, 0, trials, di2, dv3, da, dact, do2);
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(outf.data(), do2, 4 * outf.size(), hipMemcpyDeviceToHost));
+        long bad = 0, badrev = 0;
+        for (int t = 0; t < trials; ++t) {
+            std::vector<float> s(initf.begin() + (size_t)t * SLOTS, initf.begin() + (size_t)(t + 1) * SLOTS), r = s;
+            for (int l = 0; l < 64; ++l)
+                if ((act[t] >> l) & 1ull) s[a[(size_t)t * 64 + l]] = s[a[(size_t)t * 64 + l]] + vv[(size_t)t * 64 + l];
+            for (int l = 63; l >= 0; --l)
+                if ((act[t] >> l) & 1ull) r[a[(size_t)t * 64 + l]] += vv[(size_t)t * 64 + l];
+            bool ok = true, okr = true;
+            for (int i = 0; i < SLOTS; ++i) {
+                if (!same_bits32(outf[(size_t)t * SLOTS + i], s[i])) ok = false;
+                if (!same_bits32(outf[(size_t)t * SLOTS + i], r[i])) okr = false;
+            }
+            bad += !ok;
+            badrev += !okr;
+        }
+        std::printf("Q5 ds_add_f32: %d trials; mismatches vs ascending-lane order %ld, vs descending %ld\n", trials, bad, badrev);
     }
     return 0;
 }

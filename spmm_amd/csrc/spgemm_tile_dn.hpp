@@ -20,15 +20,17 @@
 
 namespace spg {
 
-// LDS atomic add with the ordering property above (f64 parts only; f32 parts keep k_tile).
-template <typename T> struct OrderedLdsAdd : std::false_type {};
-template <> struct OrderedLdsAdd<double> : std::true_type {};
-template <> struct OrderedLdsAdd<cplx<double>> : std::true_type {};
+// LDS atomic add with the ordering property above; ds_add_f32 has both properties too
+// (abtest/lds_fadd_order.hip, Q4/Q5: rounding incl. denormals, ascending lane order).
+template <typename T> struct OrderedLdsAdd : std::true_type {};
 
 __device__ __forceinline__ void lds_add(double* p, double v) {
     __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-__device__ __forceinline__ void lds_add(cplx<double>* p, cplx<double> v) {
+__device__ __forceinline__ void lds_add(float* p, float v) {
+    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+template <typename R> __device__ __forceinline__ void lds_add(cplx<R>* p, cplx<R> v) {
     lds_add(&p->re, v.re);
     lds_add(&p->im, v.im);
 }
@@ -55,7 +57,14 @@ template <typename T> struct __attribute__((aligned(16))) DnEnt {
 #ifndef SPG_DN_SENT
 #define SPG_DN_SENT 1
 #endif
-template <typename T> constexpr bool dn_sent() { return SPG_DN_SENT && std::is_same<T, double>::value; }
+template <typename T> constexpr bool dn_sent() {
+    return SPG_DN_SENT && (std::is_same<T, double>::value || std::is_same<T, float>::value);
+}
+// the -0.0 sentinel's bits and the bits of a real value
+template <typename T> __device__ __forceinline__ bool is_neg_zero(T v) {
+    if constexpr (sizeof(T) == 8) return __double_as_longlong(v) == (long long)0x8000000000000000ull;
+    else return __float_as_uint(v) == 0x80000000u;
+}
 
 template <typename T, bool HIT = !dn_sent<T>()> struct DnLds {
     T acc[DN_TW + WAVE];          // accumulator by column; + one lane-private slot per lane
@@ -70,7 +79,6 @@ template <typename T> struct DnLds<T, false> {
     uint8_t mk[NUM_MK];
 };
 
-constexpr uint64_t NEG_ZERO = 0x8000000000000000ull;
 
 // The ordered product walk of one item (row, tile): its A entries in batches of 64 (the first
 // NB batches' tile segments `sq` and values `aq` given, the rest loaded here); per batch a DPP
@@ -141,10 +149,11 @@ __device__ __forceinline__ void dn_walk(L* lp, T* acc, int l, int TWD, const int
                         const int t = gb + c0 + u * WAVE + l;
                         val[u] = u < nu && t < Pb;
                         uint32_t eb;
-                        if constexpr (sizeof(T) == 8) {   // base and value with one 16-byte read
+                        if constexpr (sizeof(T) <= 8) {   // base and value with one 16-byte read
                             const uint4 e4 = reinterpret_cast<const uint4*>(ent)[(int)max(sp[u], 1u) - 1];
                             eb = e4.x;
-                            qa[u] = __hiloint2double((int)e4.w, (int)e4.z);
+                            const uint32_t w2[2] = {e4.z, e4.w};
+                            __builtin_memcpy(&qa[u], w2, sizeof(T));
                         } else {
                             const DnEnt<T> e = ent[(int)max(sp[u], 1u) - 1];
                             eb = e.base;
@@ -192,8 +201,9 @@ __device__ __forceinline__ void dn_item(DnLds<T>& S, int l, int TW, int lo, int 
     {   // clear the accumulator (-0.0: dn_sent) and the hit bytes (16-byte stores; TW is a
         // multiple of 64)
         uint4* a4 = reinterpret_cast<uint4*>(S.acc);
-        const uint32_t hi = dn_sent<T>() ? 0x80000000u : 0u;
-        for (int q = l; q < TW * (int)sizeof(T) / 16; q += WAVE) a4[q] = make_uint4(0u, hi, 0u, hi);
+        const uint32_t hi = dn_sent<T>() ? 0x80000000u : 0u;       // -0.0's sign bit
+        const uint32_t lw = sizeof(T) == 4 ? hi : 0u;              // (fp32: every word is a value)
+        for (int q = l; q < TW * (int)sizeof(T) / 16; q += WAVE) a4[q] = make_uint4(lw, hi, lw, hi);
         if constexpr (!dn_sent<T>()) {
             uint4* h4 = reinterpret_cast<uint4*>(S.hit);
             for (int q = l; q < TW / 16; q += WAVE) h4[q] = make_uint4(0u, 0u, 0u, 0u);
@@ -212,7 +222,7 @@ __device__ __forceinline__ void dn_item(DnLds<T>& S, int l, int TW, int lo, int 
             const int c = k * WAVE + l;
             const T v = S.acc[c];
             bool h;
-            if constexpr (dn_sent<T>()) h = __double_as_longlong(v) != (long long)NEG_ZERO;
+            if constexpr (dn_sent<T>()) h = !is_neg_zero(v);
             else h = S.hit[c] != 0;
             const unsigned long long m = __ballot(h);
             if (h && (SPG_TILE_DIAG & 8) == 0) {   // (diag 8, timing only: no output)
@@ -237,7 +247,7 @@ __device__ __forceinline__ void dn_item(DnLds<T>& S, int l, int TW, int lo, int 
                         int c;
                         T v;
                         load_rec(reinterpret_cast<const uint32_t*>(rb + (uint64_t)i * RB), 0, c, v);
-                        if (__double_as_longlong(S.acc[c]) == (long long)NEG_ZERO) S.acc[c] = 0.0;
+                        if (is_neg_zero(S.acc[c])) S.acc[c] = (T)0;
                     }
                 }
             }

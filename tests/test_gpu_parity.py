@@ -642,17 +642,18 @@ def test_alg1_lb_direct_path_bitexact(tmp_path):
     _assert_same((got["p"].astype(np.int64), got["j"], got["x"]), oracle.spgemm(A, B, keep_zeros=True, sort=True))
 
 
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("frac", [1.0, 0.3])
-def test_tile_dense_negative_zero_products(frac):
+def test_tile_dense_negative_zero_products(frac, dtype):
     """Dense fp64 tiles start every accumulator slot at -0.0 and take the item's structure
     from the slots that left it (spgemm_tile_dn.hpp, dn_sent).  A column reached only by
     -0.0 products keeps -0.0 there while scipy's sum (from +0.0) is +0.0: such items take the
     re-walk path.  B values set to -0.0 (all of them, or 30 %) must still give the oracle's
     structure and +0.0 values, bit for bit."""
     from spmm_amd import gen
-    A, B = gen.scipy_pair(2048, 0.02, seed=5)
-    A.data = np.abs(A.data) + 0.5
+    A, B = gen.scipy_pair(2048, 0.02, seed=5, dtype=dtype)
+    A.data = np.abs(A.data) + dtype(0.5)
     rng = np.random.default_rng(1)
-    B.data = np.where(rng.random(B.nnz) < frac, -0.0, B.data)
+    B.data = np.where(rng.random(B.nnz) < frac, dtype(-0.0), B.data).astype(dtype)
     for alg in (1, 2):
         _assert_same(_gpu(A, B, alg=alg), oracle.spgemm(A, B, keep_zeros=True, sort=True))
