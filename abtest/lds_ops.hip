@@ -44,6 +44,12 @@ __global__ __launch_bounds__(WPB * 64) void k_ops(unsigned seed, double* sink) {
         } else if constexpr (OP == 7) {
             // two f32 halves of the column's slot (a u32 atomic add stands in for the pair)
             atomicAdd(reinterpret_cast<unsigned*>(&acc[w][0]) + 2 * c, 1u);
+        } else if constexpr (OP == 8) {
+            __hip_atomic_fetch_add(reinterpret_cast<float*>(&acc[w][0]) + c, (float)v, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else if constexpr (OP == 9) {
+            __hip_atomic_fetch_add(reinterpret_cast<float*>(&acc[w][0]) + 2 * c, (float)v, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     }
     __syncthreads();
@@ -77,11 +83,13 @@ int main() {
     (void)hipMalloc(&sink, 8);
     const double clk = p.clockRate * 1e3;   // Hz
     const char* names[] = {"ds_add_f64", "ds_write_b8 (hit)", "ds_add_f64 + ds_write_b8", "ds_read_b64+add+ds_write_b64",
-                           "ds_or_b32 (bitmap)", "ds_read_b64", "ds_add_f64 + ds_or_b32", "ds_add_u32"};
-    float t[8] = {run<0>(blocks, sink), run<1>(blocks, sink), run<2>(blocks, sink), run<3>(blocks, sink),
-                  run<4>(blocks, sink), run<5>(blocks, sink), run<6>(blocks, sink), run<7>(blocks, sink)};
+                           "ds_or_b32 (bitmap)", "ds_read_b64", "ds_add_f64 + ds_or_b32", "ds_add_u32", "ds_add_f32 (dense slots)",
+                           "ds_add_f32 (stride-2 slots)"};
+    float t[10] = {run<0>(blocks, sink), run<1>(blocks, sink), run<2>(blocks, sink), run<3>(blocks, sink),
+                   run<4>(blocks, sink), run<5>(blocks, sink), run<6>(blocks, sink), run<7>(blocks, sink),
+                   run<8>(blocks, sink), run<9>(blocks, sink)};
     const double waves_per_cu = (double)blocks * WPB / cus;
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < 10; ++i) {
         const double cyc = t[i] * 1e-3 * clk;   // cycles of the run
         std::printf("%-32s %8.3f ms  %6.2f CU-cycles per wave-instruction\n", names[i], t[i],
                     cyc / (waves_per_cu * ITERS));

@@ -48,16 +48,16 @@ def run_spmm_case(m, n, p, density, dtype, dtype_str, runs, seed, do_warmup=True
     rs = repeat_gpu(op + " [sparse, inputs_on_gpu]", lambda: A_sparse @ B_sparse, runs, do_warmup)
     rd = repeat_gpu(op + " [dense, inputs_on_gpu]", lambda: A_dense @ B_dense, runs, do_warmup)
 
-    header = f"{'name':40}  {'time(ms)':>10}  {'ΔPeak Mem':>16}  {'out_shape':>16}  {'dtype':>10}"
+    header = f"{'name':40}  {'time(ms)':>10}  {'ΔPeak Mem':>16}  {'out_shape':>16}  {'dtype':>10}  {'lib peak':>12}"
     print(header)
     print("-" * len(header))
 
     def show(r: Optional[BenchResult]):
         if r is None:
-            print(f"{'SKIPPED (OOM)':40}  {'-':>10}  {'-':>16}  {'-':>16}  {'-':>10}")
+            print(f"{'SKIPPED (OOM)':40}  {'-':>10}  {'-':>16}  {'-':>16}  {'-':>10}  {'-':>12}")
             return
         print(f"{r.name:40}  {r.time_ms:10.6f}  {human_bytes(r.peak_vram):>16}  "
-              f"{str(tuple(r.out_shape)):>16}  {str(r.out_dtype):>10}")
+              f"{str(tuple(r.out_shape)):>16}  {str(r.out_dtype):>10}  {human_bytes(r.lib_peak_bytes):>12}")
 
     show(rs)
     show(rd)

@@ -20,9 +20,14 @@
 
 namespace spg {
 
-// LDS atomic add with the ordering property above; ds_add_f32 has both properties too
-// (abtest/lds_fadd_order.hip, Q4/Q5: rounding incl. denormals, ascending lane order).
-template <typename T> struct OrderedLdsAdd : std::true_type {};
+// LDS atomic add with the ordering property above, used for fp64 and complex128.
+// ds_add_f32 has both properties too (abtest/lds_fadd_order.hip Q4/Q5), but on MI355X it
+// costs 193 CU-cycles per wave-instruction against ds_add_f64's 26 (abtest/lds_ops.hip,
+// profiles/r03_lds_ops.txt), so fp32 and complex64 keep k_tile's owner rounds: lean fp32
+// measured 28.4 ms vs k_tile's 8.45 ms numeric at N=8192, rho=0.1 (profiles/r03_ab/).
+template <typename T> struct OrderedLdsAdd : std::false_type {};
+template <> struct OrderedLdsAdd<double> : std::true_type {};
+template <> struct OrderedLdsAdd<cplx<double>> : std::true_type {};
 
 __device__ __forceinline__ void lds_add(double* p, double v) {
     __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
