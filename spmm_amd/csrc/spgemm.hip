@@ -221,7 +221,9 @@ inline bool want_tile(const spg_csr_t& A, const spg_csr_t& B, int& tws, int& G) 
     if (frac * (double)(1 << tws) < 64.0) return false;
     // the tile-major B's segment table is int32 and its records are addressed with 32-bit
     // byte offsets
-    if (B.nnz > 2147483647LL || (double)B.nnz * (double)brec_bytes(B.value_type) >= 4294967296.0) return false;
+    if (B.nnz > 2147483647LL ||
+        (double)(B.nnz + 2 * SENT_N) * (double)brec_bytes(B.value_type) >= 4294967296.0)
+        return false;
     G = (int)((B.cols + (1 << tws) - 1) >> tws);
     return (double)A.rows * G < 2.0e9;
 }
@@ -540,7 +542,8 @@ Layout make_layout(const spg_plan_s& p) {
     if (p.use_tile) {
         L.tptr = off;  off = align_up(off + sizeof(int32_t) * (size_t)(bt_entries(p) + 1));
         L.sidx = off;  off = align_up(off + sizeof(uint32_t) * (size_t)p.B.rows * (size_t)(sym_tiles(p) + 1));
-        L.brec = off;  off = align_up(off + brec_bytes(p.A.value_type) * (size_t)std::max<int64_t>(p.B.nnz, 1));
+        // (B's records, then the lean kernels' 2 * SENT_N sentinel records)
+        L.brec = off;  off = align_up(off + brec_bytes(p.A.value_type) * (size_t)(p.B.nnz + 2 * SENT_N));
         L.items = off; off = align_up(off + sizeof(int64_t) * (size_t)(tile_item_slots(p) + 1));
         // item bitmaps; before the first symbolic pass the region holds the row-major
         // boundary index the tile-major B is built from
@@ -889,10 +892,15 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
     const T* Bx = (const T*)p.B.values;
     if (!p.brec_built) {
         timed_launch(h, SPG_PHASE_SPILL, k_bt_pack<T, IP>, dim3((unsigned)grid_for(p.B.rows, 4)), dim3(256), p.B.rows,
-                     Bp, Bj, Bx, p.tws, (const int32_t*)p.tptr, (uint32_t*)p.brec);
+                     Bp, Bj, Bx, p.tws, (const int32_t*)p.tptr, (uint32_t*)p.brec, p.B.nnz);
         SPG_LAUNCHED(h);
         p.brec_built = true;
     }
+    // byte offsets of the two sentinel regions after B's records (k_bt_pack)
+    const uint32_t sent_dn = (uint32_t)((uint64_t)p.B.nnz * sizeof(uint32_t) * rec_words<T>());
+    const uint32_t sent_sp = sent_dn + (uint32_t)(SENT_N * sizeof(uint32_t) * rec_words<T>());
+    (void)sent_dn;
+    (void)sent_sp;
     const int64_t nch = tile_chunks(p);
     for (int64_t c = 0; c < nch; ++c) {
         spg_status_t st;
@@ -918,15 +926,15 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
                 hipExtLaunchKernelGGL((k_tile_sp<T, IP>), dim3(tile_grid(n * p.G, SP_WPB)), dim3(SP_WPB * WAVE), 0,
                                       h->stream, kt.a, kt.b, 0, r0, n, p.tws, p.G, Ap, Aj, Ax, p.B.rows,
                                       (const uint32_t*)p.brec, (const int32_t*)p.tptr, (const uint32_t*)p.bitmap,
-                                      (const int64_t*)tile_chunk_items(p, c), cj, cx, alpha);
+                                      (const int64_t*)tile_chunk_items(p, c), cj, cx, alpha, sent_sp);
                 SPG_LAUNCHED(h);
                 continue;
             }
-            if (dense && SPG_TILE_LEAN) {   // ordered LDS adds (spgemm_tile_dn.hpp)
+            if (dense && SPG_TILE_LEAN && (1 << p.tws) <= DN_TW) {   // ordered LDS adds (spgemm_tile_dn.hpp)
                 hipExtLaunchKernelGGL((k_tile_dn<T, IP>), dim3(tile_grid(n * p.G, DN_WPB)), dim3(DN_WPB * WAVE), 0,
                                       h->stream, kt.a, kt.b, 0, r0, n, p.tws, p.G, Ap, Aj, Ax, p.B.rows,
                                       (const uint32_t*)p.brec, (const int32_t*)p.tptr,
-                                      (const int64_t*)tile_chunk_items(p, c), cj, cx, alpha);
+                                      (const int64_t*)tile_chunk_items(p, c), cj, cx, alpha, sent_dn);
                 SPG_LAUNCHED(h);
                 continue;
             }

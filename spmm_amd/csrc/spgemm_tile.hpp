@@ -99,11 +99,13 @@ __global__ __launch_bounds__(256) void k_tile_index(int64_t rows, const IP* __re
     for (int g = tl + 1 + l; g <= G; g += WAVE) put(g, (uint32_t)len);
 }
 
-// Tile-major B records: the entry's column inside its tile (32 bits) followed by its value,
+// Tile-major B records: the entry's value followed by its column inside its tile (32 bits),
 // packed without padding -- 8 bytes (f32), 12 bytes (f64, complex64), 20 bytes
 // (complex128) -- so one dwordx2 / dwordx3 load brings both, and the slice of a tile the
-// XCD keeps in L2 is as small as the values allow.  Offsets are 32-bit byte offsets from
-// the (scalar) base: the host keeps the record array under 4 GiB on the tile path.
+// XCD keeps in L2 is as small as the values allow.  The value comes first so that an f64
+// lands in the even-aligned register pair of the dwordx3 (no moves before the multiply).
+// Offsets are 32-bit byte offsets from the (scalar) base: the host keeps the record array
+// under 4 GiB on the tile path.
 template <typename T> constexpr int rec_words() { return 1 + (int)(sizeof(T) / 4); }
 
 template <typename T, typename IP>
@@ -113,20 +115,20 @@ __device__ __forceinline__ void load_rec(const uint32_t* __restrict__ rec, IP i,
         reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(rec) + (uint64_t)((uint32_t)i * (uint32_t)(4 * W)));
     if constexpr (W == 2) {          // f32
         const uint2 x = *reinterpret_cast<const uint2*>(q);
-        lc = (int)x.x;
-        v = __uint_as_float(x.y);
+        v = __uint_as_float(x.x);
+        lc = (int)x.y;
     } else if constexpr (W == 3) {   // f64, complex64
         const uint3 x = *reinterpret_cast<const uint3*>(q);
-        lc = (int)x.x;
         if constexpr (std::is_same<T, double>::value) {
-            v = __hiloint2double((int)x.z, (int)x.y);
+            v = __hiloint2double((int)x.y, (int)x.x);
         } else {
-            v.re = __uint_as_float(x.y);
-            v.im = __uint_as_float(x.z);
+            v.re = __uint_as_float(x.x);
+            v.im = __uint_as_float(x.y);
         }
+        lc = (int)x.z;
     } else {                          // complex128
-        lc = (int)q[0];
-        __builtin_memcpy(&v, q + 1, sizeof(T));
+        __builtin_memcpy(&v, q, sizeof(T));
+        lc = (int)q[W - 1];
     }
 }
 
@@ -134,8 +136,21 @@ template <typename T>
 __device__ __forceinline__ void store_rec(uint32_t* __restrict__ rec, int64_t i, int lc, T v) {
     constexpr int W = rec_words<T>();
     uint32_t* q = rec + i * W;
-    q[0] = (uint32_t)lc;
-    __builtin_memcpy(q + 1, &v, sizeof(T));
+    __builtin_memcpy(q, &v, sizeof(T));
+    q[W - 1] = (uint32_t)lc;
+}
+
+// Sentinel records after B's nnz records: the lean tile kernels point every product slot past
+// the end of a batch at them instead of masking the slot (no compare / select per chunk).
+// Region 0 (dense tiles): columns DN_TW + (i % 32), accumulator slots nobody reads; region 1
+// (sparse tiles): columns >= 65536, outside every window.  Value 0.
+constexpr int SENT_N = 512;   // records per region: a step never runs more than 512 slots past its batch
+#ifndef SPG_DN_TW
+#define SPG_DN_TW 1024
+#endif
+constexpr int DN_TW = SPG_DN_TW;   // dense tiles: <= TILE_CAP columns, one accumulator window
+__device__ __forceinline__ int sentinel_col(int i) {
+    return i < SENT_N ? DN_TW + (i & 31) : 65536 + (i & 63);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -169,11 +184,16 @@ __global__ __launch_bounds__(256) void k_bt_count(int64_t K, int G, int R, const
 
 // One wave per B row: an entry's rank inside its tile segment is its distance to the
 // segment's first entry, found by a max-scan over the lanes where the tile id steps.
+// (The grid's first 2 * SENT_N threads also write the sentinel records after the nnz(B)
+// real ones.)
 template <typename T, typename IP>
 __global__ __launch_bounds__(256) void k_bt_pack(int64_t K, const IP* __restrict__ Bp, const int32_t* __restrict__ Bj,
                                                  const T* __restrict__ Bx, int tws,
-                                                 const int32_t* __restrict__ tptr, uint32_t* __restrict__ rec) {
+                                                 const int32_t* __restrict__ tptr, uint32_t* __restrict__ rec,
+                                                 int64_t nnzB) {
     const int l = lane_id();
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < 2 * SENT_N; i += gridDim.x * 256)
+        store_rec(rec, nnzB + i, sentinel_col(i), (T)0);
     const int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (k >= K) return;
     const IP r0 = Bp[k];

@@ -40,12 +40,15 @@ template <typename R> __device__ __forceinline__ void lds_add(cplx<R>* p, cplx<R
     lds_add(&p->im, v.im);
 }
 
-constexpr int DN_TW = 1024;   // dense tiles: <= TILE_CAP columns, one accumulator window
 constexpr int DN_WPB = 2;     // waves per block
+constexpr int DN_DUMMY = 32;  // accumulator slots past DN_TW: the dense sentinel records add into them
 
 // Per-batch A-entry table: the byte offset of the entry's first product record, shifted by
 // the entry's flattened offset (so product t of the batch reads base[src] + t * RB), and the
-// A value.  One 16-byte LDS read per product lane (f64).
+// A value.  One 16-byte LDS read per product lane (f64).  Entry WAVE is the batch's pseudo
+// entry: from product Pb on (past the batch's products, up to the end of the step) the slots
+// read the sentinel records (spgemm_tile.hpp), which add 0 into slots nobody reads -- no
+// compare, select or clamp per chunk.
 template <typename T> struct __attribute__((aligned(16))) DnEnt {
     uint32_t base;
     uint32_t pad;
@@ -72,31 +75,46 @@ template <typename T> __device__ __forceinline__ bool is_neg_zero(T v) {
 }
 
 template <typename T, bool HIT = !dn_sent<T>()> struct DnLds {
-    T acc[DN_TW + WAVE];          // accumulator by column; + one lane-private slot per lane
-    DnEnt<T> ent[WAVE];
+    T acc[DN_TW + DN_DUMMY];      // accumulator by column; + the sentinel records' slots
+    DnEnt<T> ent[WAVE + 1];
     uint8_t mk[NUM_MK];           // lane -> A-entry markers of 8 chunks
-    uint8_t hit[DN_TW + WAVE];    // columns some product reached (non-sentinel types)
+    uint8_t hit[DN_TW + DN_DUMMY];   // columns some product reached (non-sentinel types)
 };
-// (dn_sent: 10,240 bytes per wave -- 8 two-wave blocks, 16 waves, fit a CU's 160 KB)
+// (dn_sent: 10,000 bytes per wave -- 8 two-wave blocks, 16 waves, fit a CU's 160 KB)
 template <typename T> struct DnLds<T, false> {
-    T acc[DN_TW + WAVE];
-    DnEnt<T> ent[WAVE];
+    T acc[DN_TW + DN_DUMMY];
+    DnEnt<T> ent[WAVE + 1];
     uint8_t mk[NUM_MK];
 };
 
+// Markers of one group of 8 chunks (transposed as num_group_markers): entry l's first product
+// gets l + 1, and product Pb (the batch's end, if inside the group) the pseudo entry's WAVE + 1.
+__device__ __forceinline__ void dn_group_markers(uint8_t* mk, int l, int cnt, int off, int gb, int Pb) {
+    wsync();
+    reinterpret_cast<uint2*>(mk)[l] = make_uint2(0u, 0u);
+    wsync();
+    if (cnt > 0 && off >= gb && off < gb + NUM_MK) {
+        const int t = off - gb;
+        mk[((t & (WAVE - 1)) << 3) | (t >> 6)] = (uint8_t)(l + 1);
+    }
+    if (l == 0 && Pb - gb < NUM_MK) {
+        const int t = Pb - gb;
+        mk[((t & (WAVE - 1)) << 3) | (t >> 6)] = (uint8_t)(WAVE + 1);
+    }
+    wsync();
+}
 
 // The ordered product walk of one item (row, tile): its A entries in batches of 64 (the first
 // NB batches' tile segments `sq` and values `aq` given, the rest loaded here); per batch a DPP
 // scan of the segment lengths and the entry table in LDS; per group of 8 chunks the transposed
 // markers; per U chunks the lane -> entry max-scans, one 16-byte table read and one record load
 // per chunk (all in flight), then per chunk in order one multiply and one ds_add_f64 into
-// acc[slot(valid, column)] -- slot() maps a product's tile column to its accumulator slot, or
-// to DUMMY + lane (a lane-private slot: the lane adds 0) -- and hit(slot).
-template <typename T, int NB, int DUMMY, typename L, typename Slot, typename Hit>
-__device__ __forceinline__ void dn_walk(L* lp, T* acc, int l, int TWD, const int32_t* __restrict__ tp,
-                                        int64_t a0, int nA, const T (&aq)[NB], const uint2 (&sq)[NB],
-                                        const int32_t* __restrict__ Aj, const T* __restrict__ Ax,
-                                        const char* __restrict__ rb, Slot&& slot, Hit&& hit) {
+// acc[slot(column)] and hit(slot).  `sent` is the byte offset of the kernel's sentinel region.
+template <typename T, int NB, typename L, typename Slot, typename Hit>
+__device__ __forceinline__ void dn_walk(L* lp, T* acc, int l, const int32_t* __restrict__ tp, int64_t a0, int nA,
+                                        T (&aq)[NB], uint2 (&sq)[NB], const int32_t* __restrict__ Aj,
+                                        const T* __restrict__ Ax, const char* __restrict__ rb, uint32_t sent,
+                                        Slot&& slot, Hit&& hit) {
     constexpr int U = sizeof(T) > 8 ? 4 : 8;     // chunks in flight
     constexpr uint32_t RB = 4u * (uint32_t)rec_words<T>();   // bytes of one B record
     DnEnt<T>* ent = lp->ent;
@@ -106,13 +124,16 @@ __device__ __forceinline__ void dn_walk(L* lp, T* acc, int l, int TWD, const int
         uint32_t beg = 0;
         T av = (T)0;
         if (b < NB * WAVE) {
+            // the preloaded batches queue in registers: take the head, shift the rest down
+            // (static register indices: a select chain or a dynamic index costs more)
+            cnt = (int)(sq[0].y - sq[0].x);
+            beg = sq[0].x;
+            av = aq[0];
 #pragma unroll
-            for (int q = 0; q < NB; ++q)
-                if (q == (b >> 6)) {
-                    cnt = (int)(sq[q].y - sq[q].x);
-                    beg = sq[q].x;
-                    av = aq[q];
-                }
+            for (int q = 0; q + 1 < NB; ++q) {
+                sq[q] = sq[q + 1];
+                aq[q] = aq[q + 1];
+            }
         } else if (b + l < nA) {
             const uint2 se = seg_pair(tp, Aj[a0 + b + l]);
             cnt = (int)(se.y - se.x);
@@ -125,9 +146,13 @@ __device__ __forceinline__ void dn_walk(L* lp, T* acc, int l, int TWD, const int
         wsync();
         ent[l].base = beg * RB - (uint32_t)off * RB;   // wraps; base + t*RB is exact
         ent[l].a = av;
+        if (l == 0) {
+            ent[WAVE].base = sent - (uint32_t)Pb * RB;   // products Pb.. read sentinel records
+            ent[WAVE].a = (T)0;
+        }
         unsigned carry = 0u;
         for (int gb = 0; gb < Pb; gb += NUM_MK) {
-            num_group_markers(*lp, l, cnt, off, gb);
+            dn_group_markers(mk, l, cnt, off, gb, Pb);
             const int nchg = min(NUM_MK, Pb - gb);
             const uint2 m2 = reinterpret_cast<const uint2*>(mk)[l];
             const uint64_t mrow = ((uint64_t)m2.y << 32) | m2.x;
@@ -144,49 +169,37 @@ __device__ __forceinline__ void dn_walk(L* lp, T* acc, int l, int TWD, const int
                         sp[u] = max(sp[u], carry);
                         carry = (unsigned)readlane_i((int)sp[u], WAVE - 1);
                     }
-                    // every slot loads a valid record: slots past the batch's products read
-                    // its last one and add 0 into their own slot
+                    // product 0 of a batch always carries a marker, so sp >= 1; slots past the
+                    // batch's products carry the pseudo entry's
                     int qc[NU];
                     T qv[NU], qa[NU];
-                    bool val[NU];
 #pragma unroll
                     for (int u = 0; u < NU; ++u) {
-                        const int t = gb + c0 + u * WAVE + l;
-                        val[u] = u < nu && t < Pb;
+                        const uint32_t t = (uint32_t)(gb + c0 + u * WAVE + l);
                         uint32_t eb;
                         if constexpr (sizeof(T) <= 8) {   // base and value with one 16-byte read
-                            const uint4 e4 = reinterpret_cast<const uint4*>(ent)[(int)max(sp[u], 1u) - 1];
+                            const uint4 e4 = reinterpret_cast<const uint4*>(ent)[(int)sp[u] - 1];
                             eb = e4.x;
                             const uint32_t w2[2] = {e4.z, e4.w};
                             __builtin_memcpy(&qa[u], w2, sizeof(T));
                         } else {
-                            const DnEnt<T> e = ent[(int)max(sp[u], 1u) - 1];
+                            const DnEnt<T> e = ent[(int)sp[u] - 1];
                             eb = e.base;
                             qa[u] = e.a;
                         }
-                        const uint32_t o = eb + __umul24((uint32_t)min(t, Pb - 1), RB);
-                        if constexpr ((SPG_TILE_DIAG & 2) != 0) {   // timing only: no record loads
-                            qc[u] = (int)((o * 2654435761u) >> 22) & (TWD - 1);
-                            qv[u] = (T)1;
-                        } else {
-                            load_rec(reinterpret_cast<const uint32_t*>(rb + o), 0, qc[u], qv[u]);
-                        }
+                        load_rec(reinterpret_cast<const uint32_t*>(rb + (eb + __umul24(t, RB))), 0, qc[u], qv[u]);
                     }
 #pragma unroll
                     for (int u = 0; u < NU; ++u) {
-                        const int c = slot(val[u], qc[u]);
-                        const T pv = c < DUMMY ? mul_rn(qa[u], qv[u]) : (T)0;
-                        if constexpr ((SPG_TILE_DIAG & 1) == 0) {   // (diag 1: no accumulation)
-                            lds_add(&acc[c], pv);   // chunk order = issue order
-                            hit(c);
-                        } else {
-                            if (pv == (T)12345) hit(c);
-                        }
+                        const int c = slot(qc[u]);
+                        lds_add(&acc[c], mul_rn(qa[u], qv[u]));   // chunk order = issue order
+                        hit(c);
                     }
                 };
                 if (nu > 3 * U / 4) step(std::integral_constant<int, U>{});
                 else if (nu > U / 2) step(std::integral_constant<int, 3 * U / 4>{});
-                else step(std::integral_constant<int, U / 2>{});
+                else if (nu > U / 4) step(std::integral_constant<int, U / 2>{});
+                else step(std::integral_constant<int, U / 4>{});
             }
         }
     }
@@ -197,9 +210,10 @@ __device__ __forceinline__ void dn_walk(L* lp, T* acc, int l, int TWD, const int
 // or (dn_sent) the slots that left -0.0 (ballot + lane rank give positions), straight to C.
 template <typename T, int NB>
 __device__ __forceinline__ void dn_item(DnLds<T>& S, int l, int TW, int lo, int nnz, const int32_t* __restrict__ tp,
-                                        int64_t a0, int nA, const T (&aq)[NB], const uint2 (&sq)[NB],
-                                        const int32_t* __restrict__ Aj, const T* __restrict__ Ax,
-                                        const char* __restrict__ rb, int32_t* __restrict__ crow,
+                                        int64_t a0, int nA, T (&aq)[NB], uint2 (&sq)[NB],
+                                        const int32_t* __restrict__ Aj,
+                                        const T* __restrict__ Ax, const char* __restrict__ rb, uint32_t sent,
+                                        int32_t* __restrict__ crow,
                                         T* __restrict__ xrow, T alpha) {
     constexpr uint32_t RB = 4u * (uint32_t)rec_words<T>();
     wsync();
@@ -214,14 +228,13 @@ __device__ __forceinline__ void dn_item(DnLds<T>& S, int l, int TW, int lo, int 
             for (int q = l; q < TW / 16; q += WAVE) h4[q] = make_uint4(0u, 0u, 0u, 0u);
         }
     }
-    dn_walk<T, NB, DN_TW>(&S, S.acc, l, TW, tp, a0, nA, aq, sq, Aj, Ax, rb,
-                          [&](bool valid, int c) { return valid ? c : DN_TW + l; },
-                          [&](int c) {
-                              if constexpr (!dn_sent<T>()) S.hit[c] = 1;
-                          });
+    dn_walk<T, NB>(&S, S.acc, l, tp, a0, nA, aq, sq, Aj, Ax, rb, sent, [&](int c) { return c; },
+                   [&](int c) {
+                       if constexpr (!dn_sent<T>()) S.hit[c] = 1;
+                   });
     wsync();
     // the item's structure, 64 columns at a time: hit[] or (dn_sent) the non -0.0 slots
-    auto emit = [&]() {
+    auto emit = [&](auto one) {
         int run = 0;
         for (int k = 0; k < TW / WAVE; ++k) {
             const int c = k * WAVE + l;
@@ -231,15 +244,16 @@ __device__ __forceinline__ void dn_item(DnLds<T>& S, int l, int TW, int lo, int 
             else h = S.hit[c] != 0;
             const unsigned long long m = __ballot(h);
             if (h && (SPG_TILE_DIAG & 8) == 0) {   // (diag 8, timing only: no output)
-                const int p = run + lane_rank(m);
+                const uint32_t p = (uint32_t)(run + lane_rank(m));
                 crow[p] = lo + c;
-                xrow[p] = (alpha == (T)1) ? v : mul_rn(alpha, v);
+                xrow[p] = decltype(one)::value ? v : mul_rn(alpha, v);
             }
             run += (int)__popcll(m);
         }
         return run;
     };
-    const int got = emit();
+    const bool one = alpha == (T)1;
+    const int got = one ? emit(std::true_type{}) : emit(std::false_type{});
     if constexpr (dn_sent<T>()) {
         if (got < nnz && (SPG_TILE_DIAG & 9) == 0) {
             // rare: a reached column saw only -0.0 products -- its slot is still -0.0, scipy's
@@ -257,7 +271,8 @@ __device__ __forceinline__ void dn_item(DnLds<T>& S, int l, int TW, int lo, int 
                 }
             }
             wsync();
-            emit();
+            if (one) emit(std::true_type{});
+            else emit(std::false_type{});
         }
     }
 }
@@ -271,7 +286,7 @@ __global__ __launch_bounds__(DN_WPB * WAVE) void k_tile_dn(
     int64_t row0, int64_t nrows, int tws, int G, const IP* __restrict__ Ap,
     const int32_t* __restrict__ Aj, const T* __restrict__ Ax, int64_t K,
     const uint32_t* __restrict__ brec, const int32_t* __restrict__ tptr,
-    const int64_t* __restrict__ item_off, int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha) {
+    const int64_t* __restrict__ item_off, int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha, uint32_t sent) {
     static_assert(OrderedLdsAdd<T>::value, "ordered LDS add needed");
     constexpr int NB = sizeof(T) > 8 ? 4 : 8;    // A batches preloaded per item
     __shared__ __attribute__((aligned(16))) DnLds<T> lds[DN_WPB];
@@ -305,7 +320,7 @@ __global__ __launch_bounds__(DN_WPB * WAVE) void k_tile_dn(
         }
 #pragma unroll
         for (int q = 0; q < NB; ++q) sq[q] = kq[q] >= 0 ? seg_pair(tp, kq[q]) : make_uint2(0u, 0u);
-        dn_item<T, NB>(S, l, TW, g * TW, nnz, tp, a0, nA, aq, sq, Aj, Ax, rb, Cj + obase, Cx + obase, alpha);
+        dn_item<T, NB>(S, l, TW, g * TW, nnz, tp, a0, nA, aq, sq, Aj, Ax, rb, sent, Cj + obase, Cx + obase, alpha);
     }
 }
 
@@ -314,23 +329,26 @@ __global__ __launch_bounds__(DN_WPB * WAVE) void k_tile_dn(
 // is its symbolic bitmap; the accumulator is compact -- a product's slot is its column's rank
 // among the item's columns (the bitmap word's popcount prefix plus the bits below it) -- in
 // windows of at most TILE_CAP slots (an item with more entries re-walks its products once
-// per window).  The same ordered walk as the dense tiles (one ds_add_f64 per 64 products);
-// the output, 64 columns at a time from the bitmap, straight to C.
+// per window).  The same ordered walk as the dense tiles (one ds_add_f64 per 64 products).
+// Output per window: the compact accumulator is already in C order, so the values leave with
+// coalesced stores; then every lane lists its bitmap words' columns (one per set bit) into the
+// freed accumulator, and the column indices leave the same way.
 template <typename T> struct SpLds {
     T acc[TILE_CAP + WAVE];       // compact accumulator of one window; + lane-private slots
     uint2 bw[TILE_NWMAX];         // (bitmap word, popcount prefix)
-    DnEnt<T> ent[WAVE];
+    DnEnt<T> ent[WAVE + 1];
     uint8_t mk[NUM_MK];
 };
 constexpr int SP_WPB = 1;   // 11.3 KB of LDS per wave: one-wave blocks pack a CU best
 
 template <typename T, typename IP>
-__global__ __launch_bounds__(SP_WPB * WAVE) void k_tile_sp(
+__global__ __launch_bounds__(SP_WPB * WAVE) __attribute__((amdgpu_waves_per_eu(sizeof(T) > 8 ? 2 : 4))) void k_tile_sp(
     int64_t row0, int64_t nrows, int tws, int G, const IP* __restrict__ Ap,
     const int32_t* __restrict__ Aj, const T* __restrict__ Ax, int64_t K,
     const uint32_t* __restrict__ brec, const int32_t* __restrict__ tptr, const uint32_t* __restrict__ bitmap,
-    const int64_t* __restrict__ item_off, int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha) {
+    const int64_t* __restrict__ item_off, int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha, uint32_t sent) {
     static_assert(OrderedLdsAdd<T>::value, "ordered LDS add needed");
+    static_assert(sizeof(T) * (TILE_CAP + WAVE) >= 4 * TILE_CAP, "column list fits the accumulator");
     constexpr int NB = sizeof(T) > 8 ? 4 : 8;
     __shared__ __attribute__((aligned(16))) SpLds<T> lds[SP_WPB];
     const int l = lane_id();
@@ -341,6 +359,7 @@ __global__ __launch_bounds__(SP_WPB * WAVE) void k_tile_sp(
     const int wpl = (nw + WAVE - 1) / WAVE;    // words per lane (<= 2)
     const char* __restrict__ rb = reinterpret_cast<const char*>(brec);
     const uint32_t items = (uint32_t)(nrows * G);
+    const bool one = alpha == (T)1;
     for (uint32_t it = xcd_block(gridDim.x) * SP_WPB + wv; it < items; it += gridDim.x * SP_WPB) {
         const int g = (int)(it / (uint32_t)nrows);
         const int64_t row = row0 + (int64_t)(it - (uint32_t)g * (uint32_t)nrows);
@@ -364,20 +383,23 @@ __global__ __launch_bounds__(SP_WPB * WAVE) void k_tile_sp(
         const int nnz = readlane_i(pincl, WAVE - 1);
         if (nnz == 0) continue;
         const int p0 = pincl - mine;
-        int32_t kq[NB];
         T aq[NB];
         uint2 sq[NB];
+        auto preload = [&]() {
+            int32_t kq[NB];
 #pragma unroll
-        for (int q = 0; q < NB; ++q) {
-            kq[q] = -1;
-            aq[q] = (T)0;
-            if (q * WAVE + l < nA) {
-                kq[q] = Aj[a0 + q * WAVE + l];
-                aq[q] = Ax[a0 + q * WAVE + l];
+            for (int q = 0; q < NB; ++q) {
+                kq[q] = -1;
+                aq[q] = (T)0;
+                if (q * WAVE + l < nA) {
+                    kq[q] = Aj[a0 + q * WAVE + l];
+                    aq[q] = Ax[a0 + q * WAVE + l];
+                }
             }
-        }
 #pragma unroll
-        for (int q = 0; q < NB; ++q) sq[q] = kq[q] >= 0 ? seg_pair(tp, kq[q]) : make_uint2(0u, 0u);
+            for (int q = 0; q < NB; ++q) sq[q] = kq[q] >= 0 ? seg_pair(tp, kq[q]) : make_uint2(0u, 0u);
+        };
+        preload();
         const int64_t obase = item_off[item];
         wsync();
         {
@@ -402,29 +424,40 @@ __global__ __launch_bounds__(SP_WPB * WAVE) void k_tile_sp(
             const int clo = 32 * wpl * L0, chi = 32 * wpl * L1;   // window, tile-relative
             wsync();
             for (int p = l; p < wn; p += WAVE) S.acc[p] = (T)0;
-            dn_walk<T, NB, TILE_CAP>(&S, S.acc, l, TW, tp, a0, nA, aq, sq, Aj, Ax, rb,
-                                     [&](bool valid, int rc) -> int {
-                                         if (!valid || rc < clo || rc >= chi) return TILE_CAP + l;
-                                         const uint2 b = S.bw[rc >> 5];
-                                         return (int)b.y + __popc(b.x & ((1u << (rc & 31)) - 1u)) - wb;
-                                     },
-                                     [&](int) {});
+            if (L0 > 0) preload();   // (the walk consumes the queue; rare later windows reload it)
+            dn_walk<T, NB>(&S, S.acc, l, tp, a0, nA, aq, sq, Aj, Ax, rb, sent,
+                           [&](int rc) -> int {
+                               if (rc < clo || rc >= chi) return TILE_CAP + l;   // (sentinels too)
+                               const uint2 b = S.bw[rc >> 5];
+                               return (int)b.y + __popc(b.x & ((1u << (rc & 31)) - 1u)) - wb;
+                           },
+                           [&](int) {});
             wsync();
-            // the window's entries, 64 columns (one lane's wpl words) at a time
-            for (int k = L0; k < L1; ++k) {
-                const int c = 32 * wpl * k + l;   // tile-relative column of this lane
-                bool h = false;
-                int pre = 0;
-                if (c < TW) {
-                    const uint2 b = S.bw[c >> 5];
-                    h = (b.x >> (c & 31)) & 1u;
-                    pre = (int)b.y + __popc(b.x & ((1u << (c & 31)) - 1u));
+            if ((SPG_TILE_DIAG & 8) == 0) {   // (diag 8, timing only: no output)
+                // values: the window's slots are its entries in C order
+                T* __restrict__ xw = Cx + obase + wb;
+                if (one)
+                    for (int p = l; p < wn; p += WAVE) xw[p] = S.acc[p];
+                else
+                    for (int p = l; p < wn; p += WAVE) xw[p] = mul_rn(alpha, S.acc[p]);
+                wsync();
+                // columns: each window lane lists its words' set bits at their ranks
+                uint32_t* __restrict__ cl = reinterpret_cast<uint32_t*>(S.acc);
+                if (l >= L0 && l < L1) {
+                    int pos = p0 - wb;
+#pragma unroll
+                    for (int q = 0; q < 2; ++q) {
+                        uint32_t w = wd[q];
+                        const int cb = lo + 32 * (w0 + q);
+                        while (w != 0u) {
+                            cl[pos++] = (uint32_t)(cb + __builtin_ctz(w));
+                            w &= w - 1u;
+                        }
+                    }
                 }
-                if (h && (SPG_TILE_DIAG & 8) == 0) {
-                    Cj[obase + pre] = lo + c;
-                    const T v = S.acc[pre - wb];
-                    Cx[obase + pre] = (alpha == (T)1) ? v : mul_rn(alpha, v);
-                }
+                wsync();
+                int32_t* __restrict__ cw = Cj + obase + wb;
+                for (int p = l; p < wn; p += WAVE) cw[p] = (int32_t)cl[p];
             }
             L0 = L1;
         }
