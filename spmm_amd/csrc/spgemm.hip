@@ -217,20 +217,27 @@ inline bool want_tile(const spg_csr_t& A, const spg_csr_t& B, int& tws, int& G) 
         if (tw <= TILE_CAP || frac * tw <= 0.95 * TILE_CAP) tws = t;
         if (tw >= (double)B.cols) break;
     }
+    // fp64 C rows at least half dense and wide: dense tiles of 2048 columns (a 2048-slot
+    // accumulator).  Half the items, half the segment-table lookups per product; config 4
+    // measured 24.9 against 26.6 ms per product with 1024-column tiles.
+    if (B.value_type == SPG_R_64F && tws == 10 && frac >= 0.5 && B.cols >= 16384) tws = 11;
     if (SPG_TILE_TWS >= 8 && SPG_TILE_TWS <= 12) tws = SPG_TILE_TWS;   // A/B timing builds only
     if (frac * (double)(1 << tws) < 64.0) return false;
     // the tile-major B's segment table is int32 and its records are addressed with 32-bit
     // byte offsets
     if (B.nnz > 2147483647LL ||
-        (double)(B.nnz + 2 * SENT_N) * (double)brec_bytes(B.value_type) >= 4294967296.0)
+        (double)(B.nnz + SENT_REGIONS * SENT_N) * (double)brec_bytes(B.value_type) >= 4294967296.0)
         return false;
     G = (int)((B.cols + (1 << tws) - 1) >> tws);
     return (double)A.rows * G < 2.0e9;
 }
 
-// grid of a tile kernel over `tasks` wave tasks: a multiple of 8 (XCD-aware block ids)
+// grid of a tile kernel over `tasks` wave tasks: a multiple of 8 (XCD-aware block ids).  The
+// kernels stride over their tasks, so the grid is capped: its work-item count must stay below
+// 2^32 (the dispatch packet's grid size is 32-bit; 33.5M two-wave blocks failed to launch).
 inline unsigned tile_grid(int64_t tasks, int wpb = TILE_WPB) {
-    const int64_t nb = std::max<int64_t>(1, std::min<int64_t>(grid_for(tasks, wpb), 1 << 26));
+    const int64_t cap = ((int64_t)1 << 31) / ((int64_t)wpb * WAVE);
+    const int64_t nb = std::max<int64_t>(1, std::min<int64_t>(grid_for(tasks, wpb), cap));
     return (unsigned)((nb + 7) / 8 * 8);
 }
 
@@ -503,7 +510,8 @@ inline int64_t tile_items(const spg_plan_s& p) { return p.use_tile ? tile_rows_m
 // accumulation itself: no symbolic bitmaps, and every item's 8-byte offset is kept (all
 // rows, not one chunk's), so ALG3's numeric phase does not recompute its chunks' counts.
 inline bool tile_dense(const spg_plan_s& p) {
-    return p.use_tile && (1 << p.tws) <= TILE_CAP && tile_variant().dense;
+    const int cap = (p.A.value_type == SPG_R_64F && SPG_TILE_LEAN) ? DN_TW_MAX : TILE_CAP;   // (k_tile_dn<.., 2048>)
+    return p.use_tile && (1 << p.tws) <= cap && tile_variant().dense;
 }
 inline int64_t tile_item_slots(const spg_plan_s& p) { return tile_dense(p) ? p.A.rows * p.G : tile_items(p); }
 // item counts / offsets of chunk c (dense tiles: every chunk's stay, at its rows' place)
@@ -542,8 +550,8 @@ Layout make_layout(const spg_plan_s& p) {
     if (p.use_tile) {
         L.tptr = off;  off = align_up(off + sizeof(int32_t) * (size_t)(bt_entries(p) + 1));
         L.sidx = off;  off = align_up(off + sizeof(uint32_t) * (size_t)p.B.rows * (size_t)(sym_tiles(p) + 1));
-        // (B's records, then the lean kernels' 2 * SENT_N sentinel records)
-        L.brec = off;  off = align_up(off + brec_bytes(p.A.value_type) * (size_t)(p.B.nnz + 2 * SENT_N));
+        // (B's records, then the lean kernels' sentinel records)
+        L.brec = off;  off = align_up(off + brec_bytes(p.A.value_type) * (size_t)(p.B.nnz + SENT_REGIONS * SENT_N));
         L.items = off; off = align_up(off + sizeof(int64_t) * (size_t)(tile_item_slots(p) + 1));
         // item bitmaps; before the first symbolic pass the region holds the row-major
         // boundary index the tile-major B is built from
@@ -896,11 +904,10 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
         SPG_LAUNCHED(h);
         p.brec_built = true;
     }
-    // byte offsets of the two sentinel regions after B's records (k_bt_pack)
-    const uint32_t sent_dn = (uint32_t)((uint64_t)p.B.nnz * sizeof(uint32_t) * rec_words<T>());
-    const uint32_t sent_sp = sent_dn + (uint32_t)(SENT_N * sizeof(uint32_t) * rec_words<T>());
-    (void)sent_dn;
-    (void)sent_sp;
+    // byte offset of sentinel region r after B's records (k_bt_pack)
+    auto sent = [&](int r) {
+        return (uint32_t)(((uint64_t)p.B.nnz + (uint64_t)r * SENT_N) * sizeof(uint32_t) * rec_words<T>());
+    };
     const int64_t nch = tile_chunks(p);
     for (int64_t c = 0; c < nch; ++c) {
         spg_status_t st;
@@ -926,15 +933,25 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
                 hipExtLaunchKernelGGL((k_tile_sp<T, IP>), dim3(tile_grid(n * p.G, SP_WPB)), dim3(SP_WPB * WAVE), 0,
                                       h->stream, kt.a, kt.b, 0, r0, n, p.tws, p.G, Ap, Aj, Ax, p.B.rows,
                                       (const uint32_t*)p.brec, (const int32_t*)p.tptr, (const uint32_t*)p.bitmap,
-                                      (const int64_t*)tile_chunk_items(p, c), cj, cx, alpha, sent_sp);
+                                      (const int64_t*)tile_chunk_items(p, c), cj, cx, alpha, sent(2));   // (sparse tiles' region)
                 SPG_LAUNCHED(h);
                 continue;
             }
-            if (dense && SPG_TILE_LEAN && (1 << p.tws) <= DN_TW) {   // ordered LDS adds (spgemm_tile_dn.hpp)
-                hipExtLaunchKernelGGL((k_tile_dn<T, IP>), dim3(tile_grid(n * p.G, DN_WPB)), dim3(DN_WPB * WAVE), 0,
-                                      h->stream, kt.a, kt.b, 0, r0, n, p.tws, p.G, Ap, Aj, Ax, p.B.rows,
-                                      (const uint32_t*)p.brec, (const int32_t*)p.tptr,
-                                      (const int64_t*)tile_chunk_items(p, c), cj, cx, alpha, sent_dn);
+            if (dense && SPG_TILE_LEAN) {   // ordered LDS adds (spgemm_tile_dn.hpp)
+                auto dn = [&](auto twd) {
+                    constexpr int TWD = decltype(twd)::value;
+                    hipExtLaunchKernelGGL((k_tile_dn<T, IP, TWD>), dim3(tile_grid(n * p.G, DN_WPB)), dim3(DN_WPB * WAVE),
+                                          0, h->stream, kt.a, kt.b, 0, r0, n, p.tws, p.G, Ap, Aj, Ax, p.B.rows,
+                                          (const uint32_t*)p.brec, (const int32_t*)p.tptr,
+                                          (const int64_t*)tile_chunk_items(p, c), cj, cx, alpha,
+                                          sent(sentinel_region(TWD)));
+                };
+                if constexpr (std::is_same<T, double>::value) {
+                    if ((1 << p.tws) > 1024) dn(std::integral_constant<int, 2048>{});
+                    else dn(std::integral_constant<int, 1024>{});
+                } else {
+                    dn(std::integral_constant<int, 1024>{});
+                }
                 SPG_LAUNCHED(h);
                 continue;
             }

@@ -142,16 +142,18 @@ __device__ __forceinline__ void store_rec(uint32_t* __restrict__ rec, int64_t i,
 
 // Sentinel records after B's nnz records: the lean tile kernels point every product slot past
 // the end of a batch at them instead of masking the slot (no compare / select per chunk).
-// Region 0 (dense tiles): columns DN_TW + (i % 32), accumulator slots nobody reads; region 1
-// (sparse tiles): columns >= 65536, outside every window.  Value 0.
-constexpr int SENT_N = 512;   // records per region: a step never runs more than 512 slots past its batch
-#ifndef SPG_DN_TW
-#define SPG_DN_TW 1024
-#endif
-constexpr int DN_TW = SPG_DN_TW;   // dense tiles: <= TILE_CAP columns, one accumulator window
+// Regions 0 and 1 (dense tiles of 1024 / 2048 columns): columns 1024 / 2048 + (i % 32),
+// accumulator slots nobody reads; region 2 (sparse tiles): columns >= 65536, outside every
+// window.  Value 0.
+constexpr int SENT_N = 512;        // records per region: a step never runs more than 512 slots past its batch
+constexpr int SENT_REGIONS = 3;
+constexpr int DN_DUMMY = 32;       // accumulator slots past a dense tile: the sentinel records add into them
+constexpr int DN_TW_MAX = 2048;    // widest dense tile (fp64: 2048-slot accumulator)
 __device__ __forceinline__ int sentinel_col(int i) {
-    return i < SENT_N ? DN_TW + (i & 31) : 65536 + (i & 63);
+    const int r = i / SENT_N, x = i % SENT_N;
+    return r == 0 ? 1024 + (x & (DN_DUMMY - 1)) : r == 1 ? 2048 + (x & (DN_DUMMY - 1)) : 65536 + (x & 63);
 }
+__host__ __device__ constexpr int sentinel_region(int dense_tw) { return dense_tw == 1024 ? 0 : dense_tw == 2048 ? 1 : 2; }
 
 // ---------------------------------------------------------------------------------------
 // Tile-major B.  For every numeric tile g, B's entries with columns in g, row by row: a CSR
@@ -184,15 +186,15 @@ __global__ __launch_bounds__(256) void k_bt_count(int64_t K, int G, int R, const
 
 // One wave per B row: an entry's rank inside its tile segment is its distance to the
 // segment's first entry, found by a max-scan over the lanes where the tile id steps.
-// (The grid's first 2 * SENT_N threads also write the sentinel records after the nnz(B)
-// real ones.)
+// (The grid's first SENT_REGIONS * SENT_N threads also write the sentinel records after the
+// nnz(B) real ones.)
 template <typename T, typename IP>
 __global__ __launch_bounds__(256) void k_bt_pack(int64_t K, const IP* __restrict__ Bp, const int32_t* __restrict__ Bj,
                                                  const T* __restrict__ Bx, int tws,
                                                  const int32_t* __restrict__ tptr, uint32_t* __restrict__ rec,
                                                  int64_t nnzB) {
     const int l = lane_id();
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < 2 * SENT_N; i += gridDim.x * 256)
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < SENT_REGIONS * SENT_N; i += gridDim.x * 256)
         store_rec(rec, nnzB + i, sentinel_col(i), (T)0);
     const int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (k >= K) return;

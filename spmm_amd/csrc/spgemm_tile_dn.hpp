@@ -40,8 +40,32 @@ template <typename R> __device__ __forceinline__ void lds_add(cplx<R>* p, cplx<R
     lds_add(&p->im, v.im);
 }
 
+// C's stores and the streamed per-item reads (A rows, item offsets) with or without the
+// non-temporal hint (SPG_NT_C / SPG_NT_A, A/B builds), so they do not push the tile's B
+// slice out of the XCD's L2.
+#ifndef SPG_NT_C
+#define SPG_NT_C 1
+#endif
+#ifndef SPG_NT_A
+#define SPG_NT_A 0
+#endif
+template <typename T> __device__ __forceinline__ void st_c(T* p, T v) {
+    if constexpr (SPG_NT_C != 0 && (sizeof(T) == 4 || sizeof(T) == 8)) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+template <typename R> __device__ __forceinline__ void st_c(cplx<R>* p, cplx<R> v) {
+    st_c(&p->re, v.re);
+    st_c(&p->im, v.im);
+}
+template <typename T> __device__ __forceinline__ T ld_a(const T* p) {
+    if constexpr (SPG_NT_A != 0 && (sizeof(T) == 4 || sizeof(T) == 8)) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <typename R> __device__ __forceinline__ cplx<R> ld_a(const cplx<R>* p) {
+    return cplx<R>(ld_a(&p->re), ld_a(&p->im));
+}
+
 constexpr int DN_WPB = 2;     // waves per block
-constexpr int DN_DUMMY = 32;  // accumulator slots past DN_TW: the dense sentinel records add into them
 
 // Per-batch A-entry table: the byte offset of the entry's first product record, shifted by
 // the entry's flattened offset (so product t of the batch reads base[src] + t * RB), and the
@@ -74,17 +98,21 @@ template <typename T> __device__ __forceinline__ bool is_neg_zero(T v) {
     else return __float_as_uint(v) == 0x80000000u;
 }
 
-template <typename T, bool HIT = !dn_sent<T>()> struct DnLds {
-    T acc[DN_TW + DN_DUMMY];      // accumulator by column; + the sentinel records' slots
+template <typename T, int TWD, bool HIT = !dn_sent<T>()> struct DnLds {
+    T acc[TWD + DN_DUMMY];        // accumulator by column; + the sentinel records' slots
     DnEnt<T> ent[WAVE + 1];
     uint8_t mk[NUM_MK];           // lane -> A-entry markers of 8 chunks
-    uint8_t hit[DN_TW + DN_DUMMY];   // columns some product reached (non-sentinel types)
+    uint8_t hit[TWD + DN_DUMMY];  // columns some product reached (non-sentinel types)
 };
-// (dn_sent: 10,000 bytes per wave -- 8 two-wave blocks, 16 waves, fit a CU's 160 KB)
-template <typename T> struct DnLds<T, false> {
-    T acc[DN_TW + DN_DUMMY];
+// (dn_sent, TWD 1024: 10,000 bytes per wave -- 8 two-wave blocks, 16 waves, fit a CU's 160 KB;
+// TWD 2048: 18,192 bytes, 8 waves)
+template <typename T, int TWD> struct DnLds<T, TWD, false> {
+    T acc[TWD + DN_DUMMY];
     DnEnt<T> ent[WAVE + 1];
     uint8_t mk[NUM_MK];
+#ifdef SPG_LDS_PAD
+    uint8_t pad[SPG_LDS_PAD];   // (A/B builds: occupancy sensitivity)
+#endif
 };
 
 // Markers of one group of 8 chunks (transposed as num_group_markers): entry l's first product
@@ -187,13 +215,24 @@ __device__ __forceinline__ void dn_walk(L* lp, T* acc, int l, const int32_t* __r
                             eb = e.base;
                             qa[u] = e.a;
                         }
-                        load_rec(reinterpret_cast<const uint32_t*>(rb + (eb + __umul24(t, RB))), 0, qc[u], qv[u]);
+                        if constexpr ((SPG_TILE_DIAG & 2) != 0) {   // timing only: no record loads
+                            qc[u] = (int)(((eb + t * 2654435761u) >> 22) & 1023u);
+                            qv[u] = (T)1;
+                        } else {
+                            load_rec(reinterpret_cast<const uint32_t*>(rb + (eb + __umul24(t, RB))), 0, qc[u], qv[u]);
+                        }
                     }
 #pragma unroll
                     for (int u = 0; u < NU; ++u) {
                         const int c = slot(qc[u]);
-                        lds_add(&acc[c], mul_rn(qa[u], qv[u]));   // chunk order = issue order
-                        hit(c);
+                        if constexpr ((SPG_TILE_DIAG & 16) != 0) {   // timing only: plain LDS stores
+                            acc[c] = mul_rn(qa[u], qv[u]);
+                        } else if constexpr ((SPG_TILE_DIAG & 32) != 0) {   // timing only: conflict-free adds
+                            lds_add(&acc[l + (c & 1)], mul_rn(qa[u], qv[u]));
+                        } else if constexpr ((SPG_TILE_DIAG & 1) == 0) {   // (diag 1, timing only: no accumulation)
+                            lds_add(&acc[c], mul_rn(qa[u], qv[u]));   // chunk order = issue order
+                            hit(c);
+                        }
                     }
                 };
                 if (nu > 3 * U / 4) step(std::integral_constant<int, U>{});
@@ -208,8 +247,8 @@ __device__ __forceinline__ void dn_walk(L* lp, T* acc, int l, const int32_t* __r
 // One dense-tile item (row, tile g of TW <= 1024 columns) on one wave: clear the accumulator,
 // the ordered product walk with slot = column, then the output 64 columns at a time from hit[]
 // or (dn_sent) the slots that left -0.0 (ballot + lane rank give positions), straight to C.
-template <typename T, int NB>
-__device__ __forceinline__ void dn_item(DnLds<T>& S, int l, int TW, int lo, int nnz, const int32_t* __restrict__ tp,
+template <typename T, int NB, int TWD>
+__device__ __forceinline__ void dn_item(DnLds<T, TWD>& S, int l, int TW, int lo, int nnz, const int32_t* __restrict__ tp,
                                         int64_t a0, int nA, T (&aq)[NB], uint2 (&sq)[NB],
                                         const int32_t* __restrict__ Aj,
                                         const T* __restrict__ Ax, const char* __restrict__ rb, uint32_t sent,
@@ -234,21 +273,29 @@ __device__ __forceinline__ void dn_item(DnLds<T>& S, int l, int TW, int lo, int 
                    });
     wsync();
     // the item's structure, 64 columns at a time: hit[] or (dn_sent) the non -0.0 slots
+    // (4 column groups per round: their LDS reads in flight together, TW >= 256)
     auto emit = [&](auto one) {
         int run = 0;
-        for (int k = 0; k < TW / WAVE; ++k) {
-            const int c = k * WAVE + l;
-            const T v = S.acc[c];
-            bool h;
-            if constexpr (dn_sent<T>()) h = !is_neg_zero(v);
-            else h = S.hit[c] != 0;
-            const unsigned long long m = __ballot(h);
-            if (h && (SPG_TILE_DIAG & 8) == 0) {   // (diag 8, timing only: no output)
-                const uint32_t p = (uint32_t)(run + lane_rank(m));
-                crow[p] = lo + c;
-                xrow[p] = decltype(one)::value ? v : mul_rn(alpha, v);
+        for (int k0 = 0; k0 < TW / WAVE; k0 += 4) {
+            T v[4];
+            bool h[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int c = (k0 + e) * WAVE + l;
+                v[e] = S.acc[c];
+                if constexpr (dn_sent<T>()) h[e] = !is_neg_zero(v[e]);
+                else h[e] = S.hit[c] != 0;
             }
-            run += (int)__popcll(m);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const unsigned long long m = __ballot(h[e]);
+                if (h[e] && (SPG_TILE_DIAG & 8) == 0) {   // (diag 8, timing only: no output)
+                    const uint32_t p = (uint32_t)(run + lane_rank(m));
+                    st_c(crow + p, (int32_t)(lo + (k0 + e) * WAVE + l));
+                    st_c(xrow + p, decltype(one)::value ? v[e] : mul_rn(alpha, v[e]));
+                }
+                run += (int)__popcll(m);
+            }
         }
         return run;
     };
@@ -281,7 +328,7 @@ __device__ __forceinline__ void dn_item(DnLds<T>& S, int l, int TW, int lo, int 
 // XCD-aware block map (an XCD works through one tile at a time, so the tile's B slice and
 // segment table stay in its L2), the first NB batches' A entries and tile segments loaded up
 // front.
-template <typename T, typename IP>
+template <typename T, typename IP, int TWD>
 __global__ __launch_bounds__(DN_WPB * WAVE) void k_tile_dn(
     int64_t row0, int64_t nrows, int tws, int G, const IP* __restrict__ Ap,
     const int32_t* __restrict__ Aj, const T* __restrict__ Ax, int64_t K,
@@ -289,10 +336,10 @@ __global__ __launch_bounds__(DN_WPB * WAVE) void k_tile_dn(
     const int64_t* __restrict__ item_off, int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha, uint32_t sent) {
     static_assert(OrderedLdsAdd<T>::value, "ordered LDS add needed");
     constexpr int NB = sizeof(T) > 8 ? 4 : 8;    // A batches preloaded per item
-    __shared__ __attribute__((aligned(16))) DnLds<T> lds[DN_WPB];
+    __shared__ __attribute__((aligned(16))) DnLds<T, TWD> lds[DN_WPB];
     const int l = lane_id();
     const int wv = uniform((int)(threadIdx.x >> 6));
-    DnLds<T>& S = lds[wv];
+    DnLds<T, TWD>& S = lds[wv];
     const int TW = 1 << tws;
     const char* __restrict__ rb = reinterpret_cast<const char*>(brec);
     const uint32_t items = (uint32_t)(nrows * G);   // host keeps rows*G < 2^31
@@ -300,8 +347,8 @@ __global__ __launch_bounds__(DN_WPB * WAVE) void k_tile_dn(
         const int g = (int)(it / (uint32_t)nrows);
         const int64_t row = row0 + (int64_t)(it - (uint32_t)g * (uint32_t)nrows);
         const int64_t item = (row - row0) * G + g;
-        const int64_t obase = item_off[item];
-        const int nnz = (int)(item_off[item + 1] - obase);
+        const int64_t obase = ld_a(item_off + item);
+        const int nnz = (int)(ld_a(item_off + item + 1) - obase);
         if (nnz == 0) continue;                      // (no product reaches this tile)
         const int32_t* __restrict__ tp = tptr + (int64_t)g * (K + 1);
         const int64_t a0 = Ap[row];
@@ -314,13 +361,13 @@ __global__ __launch_bounds__(DN_WPB * WAVE) void k_tile_dn(
             kq[q] = -1;
             aq[q] = (T)0;
             if (q * WAVE + l < nA) {
-                kq[q] = Aj[a0 + q * WAVE + l];
-                aq[q] = Ax[a0 + q * WAVE + l];
+                kq[q] = ld_a(Aj + a0 + q * WAVE + l);
+                aq[q] = ld_a(Ax + a0 + q * WAVE + l);
             }
         }
 #pragma unroll
         for (int q = 0; q < NB; ++q) sq[q] = kq[q] >= 0 ? seg_pair(tp, kq[q]) : make_uint2(0u, 0u);
-        dn_item<T, NB>(S, l, TW, g * TW, nnz, tp, a0, nA, aq, sq, Aj, Ax, rb, sent, Cj + obase, Cx + obase, alpha);
+        dn_item<T, NB, TWD>(S, l, TW, g * TW, nnz, tp, a0, nA, aq, sq, Aj, Ax, rb, sent, Cj + obase, Cx + obase, alpha);
     }
 }
 
@@ -338,6 +385,9 @@ template <typename T> struct SpLds {
     uint2 bw[TILE_NWMAX];         // (bitmap word, popcount prefix)
     DnEnt<T> ent[WAVE + 1];
     uint8_t mk[NUM_MK];
+#ifdef SPG_LDS_PAD
+    uint8_t pad[SPG_LDS_PAD];   // (A/B builds: occupancy sensitivity)
+#endif
 };
 constexpr int SP_WPB = 1;   // 11.3 KB of LDS per wave: one-wave blocks pack a CU best
 
@@ -392,8 +442,8 @@ __global__ __launch_bounds__(SP_WPB * WAVE) __attribute__((amdgpu_waves_per_eu(s
                 kq[q] = -1;
                 aq[q] = (T)0;
                 if (q * WAVE + l < nA) {
-                    kq[q] = Aj[a0 + q * WAVE + l];
-                    aq[q] = Ax[a0 + q * WAVE + l];
+                    kq[q] = ld_a(Aj + a0 + q * WAVE + l);
+                    aq[q] = ld_a(Ax + a0 + q * WAVE + l);
                 }
             }
 #pragma unroll
@@ -436,10 +486,20 @@ __global__ __launch_bounds__(SP_WPB * WAVE) __attribute__((amdgpu_waves_per_eu(s
             if ((SPG_TILE_DIAG & 8) == 0) {   // (diag 8, timing only: no output)
                 // values: the window's slots are its entries in C order
                 T* __restrict__ xw = Cx + obase + wb;
-                if (one)
-                    for (int p = l; p < wn; p += WAVE) xw[p] = S.acc[p];
-                else
-                    for (int p = l; p < wn; p += WAVE) xw[p] = mul_rn(alpha, S.acc[p]);
+                auto vals = [&](auto one) {   // 4 rows of 64 slots per round, reads first
+                    for (int p0 = 0; p0 < wn; p0 += 4 * WAVE) {
+                        T v[4];
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) v[e] = S.acc[min(p0 + e * WAVE + l, TILE_CAP + WAVE - 1)];
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const int p = p0 + e * WAVE + l;
+                            if (p < wn) st_c(xw + p, decltype(one)::value ? v[e] : mul_rn(alpha, v[e]));
+                        }
+                    }
+                };
+                if (one) vals(std::true_type{});
+                else vals(std::false_type{});
                 wsync();
                 // columns: each window lane lists its words' set bits at their ranks
                 uint32_t* __restrict__ cl = reinterpret_cast<uint32_t*>(S.acc);
@@ -457,7 +517,16 @@ __global__ __launch_bounds__(SP_WPB * WAVE) __attribute__((amdgpu_waves_per_eu(s
                 }
                 wsync();
                 int32_t* __restrict__ cw = Cj + obase + wb;
-                for (int p = l; p < wn; p += WAVE) cw[p] = (int32_t)cl[p];
+                for (int p0 = 0; p0 < wn; p0 += 4 * WAVE) {
+                    uint32_t v[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = cl[min(p0 + e * WAVE + l, TILE_CAP - 1)];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int p = p0 + e * WAVE + l;
+                        if (p < wn) st_c(cw + p, (int32_t)v[e]);
+                    }
+                }
             }
             L0 = L1;
         }

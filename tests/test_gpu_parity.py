@@ -295,6 +295,34 @@ def test_tile_path_windows_and_skew():
         _assert_same(_gpu(A, B, alg=alg, alpha=-0.75, cf=cf), ref)
 
 
+@pytest.mark.parametrize("neg", [False, True])
+def test_tile_path_dense_2048(neg):
+    """fp64 C rows over half dense and >= 16384 columns take 2048-column dense tiles
+    (k_tile_dn<double, .., 2048>; config 4's shape): a ragged last tile, an empty A row, B
+    with empty rows, every algorithm with ALG3's chunks forced; `neg` sets 30 % of B's values
+    to -0.0 (the accumulator's -0.0 start and its re-walk).  plan_info confirms the width."""
+    from spmm_amd import cusparse
+    from spmm_amd.sparse import csr_matrix
+    rng = np.random.default_rng(33)
+    A = sp.random(257, 17000, density=0.01, format="lil", random_state=rng, dtype=np.float64)
+    A[5, :] = 0
+    A = sp.csr_matrix(A)
+    B = sp.random(17000, 17000, density=0.01, format="lil", random_state=rng, dtype=np.float64)
+    B[100:140, :] = 0
+    B = sp.csr_matrix(B)
+    if neg:
+        A.data = np.abs(A.data) + 0.5
+        B.data = np.where(rng.random(B.nnz) < 0.3, -0.0, B.data)
+    for M in (A, B):
+        M.sort_indices()
+    ref = oracle.spgemm(A, B, keep_zeros=True, sort=True)
+    dA, dB = csr_matrix(A, device=_dev()), csr_matrix(B, device=_dev())
+    info = cusparse.plan_info(dA, dB, alg=2)
+    assert info["tile_width"] == 2048 and info["dense_tiles"], info
+    for alg, cf in [(1, 0.2), (2, 0.2), ("3c", 0.1)]:
+        _assert_same(_gpu(A, B, alg=alg, cf=cf), ref)
+
+
 def test_tile_path_dense_tiles_fp32_int64():
     """1024-column tiles over a dense C (batches of 64 A entries with > 1024 products per
     batch and tile), fp32 values, int64 row pointers, B with empty rows."""
