@@ -106,6 +106,7 @@ struct spg_plan_s {
     int32_t* tptr = nullptr;        // tile-major B: segment table, G * (B.rows + 1)
     uint32_t* sidx = nullptr;       // symbolic-tile starts inside each B row, B.rows * (Gs + 1)
     void* brec = nullptr;           // tile-major B: (column, value) records (numeric tile pass)
+    uint16_t* bj16 = nullptr;       // B's columns modulo 65536 (symbolic tile pass)
     bool brec_built = false;
     uint32_t* bitmap = nullptr;     // per-item column bitmaps (symbolic -> numeric)
     int64_t* item_cnt = nullptr;    // per-item counts, scanned in place into offsets
@@ -488,7 +489,7 @@ spg_status_t read_scalars(spg_handle_t h, const int64_t* dev, int n, int64_t* ou
 
 struct Layout {
     size_t scalars = 0, row_cnt = 0, seg = 0, spill = 0, status = 0, ub = 0, tj = 0, tx = 0;
-    size_t tptr = 0, sidx = 0, items = 0, bitmap = 0, brec = 0, ext = 0, total = 0;
+    size_t tptr = 0, sidx = 0, items = 0, bitmap = 0, brec = 0, bj16 = 0, ext = 0, total = 0;
 };
 
 // Tile path row chunks: ALG3's chunks (items and bitmaps are sized by the largest one and
@@ -553,6 +554,9 @@ Layout make_layout(const spg_plan_s& p) {
         // (B's records, then the lean kernels' sentinel records)
         L.brec = off;  off = align_up(off + brec_bytes(p.A.value_type) * (size_t)(p.B.nnz + SENT_REGIONS * SENT_N));
         L.items = off; off = align_up(off + sizeof(int64_t) * (size_t)(tile_item_slots(p) + 1));
+        // B's column indices modulo 65536 (the symbolic pass's columns: a symbolic tile never
+        // crosses a 65536-aligned block)
+        L.bj16 = off;  off = align_up(off + sizeof(uint16_t) * (size_t)std::max<int64_t>(p.B.nnz, 1));
         // item bitmaps; before the first symbolic pass the region holds the row-major
         // boundary index the tile-major B is built from
         const size_t bm = tile_dense(p) ? 0 : sizeof(uint32_t) * (size_t)tile_items(p) * (size_t)((1 << p.tws) >> 5);
@@ -587,6 +591,7 @@ void carve(spg_plan_s& p, const Layout& L) {
         p.sidx = (uint32_t*)(p.ws + L.sidx);
         p.tidx = (uint2*)(p.ws + L.bitmap);
         p.brec = (void*)(p.ws + L.brec);
+        p.bj16 = (uint16_t*)(p.ws + L.bj16);
         p.item_cnt = (int64_t*)(p.ws + L.items);
         p.bitmap = (uint32_t*)(p.ws + L.bitmap);
     }
@@ -821,6 +826,10 @@ spg_status_t tile_build_index(spg_handle_t h, spg_plan_s& p) {
                      dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(grid_for(n2, 256), 65536))), dim3(256),
                      p.B.rows, p.G, R, (const uint2*)p.tidx, p.tptr, p.sidx);
         SPG_LAUNCHED(h);
+        timed_launch(h, SPG_PHASE_SPILL, k_bj16,
+                     dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(grid_for(p.B.nnz, 256), 65536))), dim3(256),
+                     p.B.nnz, Bj, p.bj16);
+        SPG_LAUNCHED(h);
     }
     spg_status_t st = launch_scan<int32_t, int32_t>(h, bt_entries(p), p.tptr, p.tptr, bt_scan_status(p),
                                                     p.scalars + 2, false);
@@ -841,12 +850,12 @@ spg_status_t tile_sym_chunk(spg_handle_t h, spg_plan_s& p, int64_t c) {
         if (p.sym_seg)
             timed_launch(h, SPG_PHASE_SYMBOLIC, k_tile_sym_seg<IP>, dim3(tile_grid(n * sym_tiles(p), SEG_WPB)),
                          dim3(SEG_WPB * WAVE), r0, n, p.tws, p.G, p.twss, (const IP*)p.A.indptr,
-                         (const int32_t*)p.A.indices, (const IP*)p.B.indptr, (const int32_t*)p.B.indices,
+                         (const int32_t*)p.A.indices, (const IP*)p.B.indptr, (const uint16_t*)p.bj16,
                          (const uint32_t*)p.sidx, tile_dense(p) ? (uint32_t*)nullptr : p.bitmap, items);
         else
             timed_launch(h, SPG_PHASE_SYMBOLIC, k_tile_sym<IP>, dim3(tile_grid(n * sym_tiles(p))), dim3(TILE_WPB * WAVE),
                          r0, n, p.tws, p.G, p.twss, (const IP*)p.A.indptr, (const int32_t*)p.A.indices,
-                         (const IP*)p.B.indptr, (const int32_t*)p.B.indices, (const uint32_t*)p.sidx,
+                         (const IP*)p.B.indptr, (const uint16_t*)p.bj16, (const uint32_t*)p.sidx,
                          tile_dense(p) ? (uint32_t*)nullptr : p.bitmap, items);
         SPG_LAUNCHED(h);
     }

@@ -270,9 +270,9 @@ __device__ __forceinline__ uint64_t marker_bytes(uint4 m, int cb) {
 // Chunks of one group (<= 16 x 64 products) U at a time: map lanes to A entries for U
 // chunks, issue all their column loads, then hand each chunk to `fn(col)` in order (lanes
 // past the group's products get col = -1).
-template <int U, typename IP, typename L, typename F>
+template <int U, typename IP, typename CT, typename L, typename F>
 __device__ __forceinline__ void walk_group(L& S, int l, int gb, int Pb, unsigned& carry,
-                                           const int32_t* __restrict__ Bj, F&& fn) {
+                                           const CT* __restrict__ Bj, F&& fn) {
     const int nchg = min(TILE_MK, Pb - gb);
     const uint4 mrow = reinterpret_cast<const uint4*>(S.mk)[l];
     for (int c0 = 0; c0 < nchg; c0 += U * WAVE) {
@@ -292,21 +292,30 @@ __device__ __forceinline__ void walk_group(L& S, int l, int gb, int Pb, unsigned
         }
         int col[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) col[u] = idx[u] >= 0 ? Bj[idx[u]] : -1;
+        for (int u = 0; u < U; ++u) col[u] = idx[u] >= 0 ? (int)Bj[idx[u]] : -1;
 #pragma unroll
         for (int u = 0; u < U; ++u)
             if (c0 + u * WAVE < nchg) fn(col[u]);
     }
 }
 
+// B's column indices modulo 65536, 2 bytes each: the symbolic passes read these instead of the
+// 4-byte indices (half the bytes of the column gathers).  A symbolic tile is at most 65536
+// columns wide and aligned to its width, so it never crosses a 65536-aligned block and a
+// column's offset inside it is (col & 0xffff) - (lo & 0xffff).
+__global__ __launch_bounds__(256) void k_bj16(int64_t nnz, const int32_t* __restrict__ Bj, uint16_t* __restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nnz; i += (int64_t)gridDim.x * 256)
+        out[i] = (uint16_t)(Bj[i] & 0xffff);
+}
+
 // Symbolic pass of the tile path over wide symbolic tiles: R = 2^(twss - tws) numeric
 // tiles at once (up to 65536 columns, the whole row for N <= 65536), so B rows are read in
 // long coalesced segments.  Writes each numeric tile's bitmap (contiguous per row) and its
-// entry count.
+// entry count.  Columns come from Bj16 (k_bj16).
 template <typename IP>
 __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile_sym(
     int64_t row0, int64_t nrows, int tws, int G, int twss, const IP* __restrict__ Ap,
-    const int32_t* __restrict__ Aj, const IP* __restrict__ Bp, const int32_t* __restrict__ Bj,
+    const int32_t* __restrict__ Aj, const IP* __restrict__ Bp, const uint16_t* __restrict__ Bj16,
     const uint32_t* __restrict__ sidx, uint32_t* __restrict__ bitmap, int64_t* __restrict__ item_cnt) {
     __shared__ __attribute__((aligned(16))) SymLds<IP> lds[TILE_WPB];
     const int l = lane_id();
@@ -321,7 +330,7 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile_sym(
         const int64_t row = row0 + (int64_t)(task / (uint32_t)Gs);
         const int gs = (int)(task % (uint32_t)Gs);
         const int t0 = gs * R, t1 = min(G, t0 + R);
-        const int lo = t0 << tws;
+        const int lo16 = (t0 << tws) & 0xffff;   // the tile's start inside its 65536-column block
         const int nws = (t1 - t0) * nw;
         const int64_t a0 = Ap[row];
         const int nA = (int)(Ap[row + 1] - a0);
@@ -357,8 +366,8 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile_sym(
             unsigned carry = 0u;
             for (int gb = 0; gb < Pb; gb += TILE_MK) {
                 group_markers(S, l, cnt, off, gb);
-                walk_group<8, IP>(S, l, gb, Pb, carry, Bj, [&](int c) {
-                    if (c >= 0) set_bit(S.bits, c - lo);
+                walk_group<8, IP>(S, l, gb, Pb, carry, Bj16, [&](int c) {
+                    if (c >= 0) set_bit(S.bits, c - lo16);
                 });
             }
         }

@@ -537,7 +537,7 @@ __global__ __launch_bounds__(SP_WPB * WAVE) __attribute__((amdgpu_waves_per_eu(s
 // Symbolic pass over long B segments (a symbolic tile's expected segment >= SEG_MIN = 128 entries:
 // config 4's whole rows of 328 columns).  The bitmap OR is order-free, so there is no lane ->
 // product map: four A entries per instruction, one per 16-lane group, each group walking its
-// entry's B segment 16 columns (64 bytes, one cache line) at a time, 8 steps in flight.
+// entry's B segment 16 columns (32 bytes of the 2-byte columns, k_bj16) at a time, 8 steps in flight.
 // Writes each numeric tile's entry count (and, for sparse numeric tiles, its bitmap), as
 // k_tile_sym.  (Measured on config 4: 4.05 ms against 7.05 ms for k_tile_sym's flattened
 // walk over 16384-column tiles and 7.0 ms for a one-entry-per-instruction cursor walk.)
@@ -545,7 +545,7 @@ constexpr int SEG_WPB = 2;
 template <typename IP>
 __global__ __launch_bounds__(SEG_WPB * WAVE) void k_tile_sym_seg(
     int64_t row0, int64_t nrows, int tws, int G, int twss, const IP* __restrict__ Ap,
-    const int32_t* __restrict__ Aj, const IP* __restrict__ Bp, const int32_t* __restrict__ Bj,
+    const int32_t* __restrict__ Aj, const IP* __restrict__ Bp, const uint16_t* __restrict__ Bj16,
     const uint32_t* __restrict__ sidx, uint32_t* __restrict__ bitmap, int64_t* __restrict__ item_cnt) {
     constexpr int U = 8;
     __shared__ __attribute__((aligned(16))) uint32_t bits_all[SEG_WPB][SYM_NWMAX];
@@ -562,7 +562,7 @@ __global__ __launch_bounds__(SEG_WPB * WAVE) void k_tile_sym_seg(
         const int64_t row = row0 + (int64_t)(task / (uint32_t)Gs);
         const int gs = (int)(task % (uint32_t)Gs);
         const int t0 = gs * R, t1 = min(G, t0 + R);
-        const int lo = t0 << tws;
+        const int lo16 = (t0 << tws) & 0xffff;   // the tile's start inside its 65536-column block
         const int nws = (t1 - t0) * nw;
         const int64_t a0 = Ap[row];
         const int nA = (int)(Ap[row + 1] - a0);
@@ -599,11 +599,11 @@ __global__ __launch_bounds__(SEG_WPB * WAVE) void k_tile_sym_seg(
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const int x = e + 16 * u + sub;
-                    col[u] = x < cnt ? Bj[beg + x] : -1;
+                    col[u] = x < cnt ? (int)Bj16[beg + x] : -1;
                 }
 #pragma unroll
                 for (int u = 0; u < U; ++u)
-                    if (col[u] >= 0) set_bit(bits, col[u] - lo);
+                    if (col[u] >= 0) set_bit(bits, col[u] - lo16);
             }
         }
         wsync();
