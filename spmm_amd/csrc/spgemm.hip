@@ -222,7 +222,13 @@ inline bool want_tile(const spg_csr_t& A, const spg_csr_t& B, int& tws, int& G) 
     // accumulator).  Half the items, half the segment-table lookups per product; config 4
     // measured 24.9 against 26.6 ms per product with 1024-column tiles.
     if (B.value_type == SPG_R_64F && tws == 10 && frac >= 0.5 && B.cols >= 16384) tws = 11;
-    if (SPG_TILE_TWS >= 8 && SPG_TILE_TWS <= 12) tws = SPG_TILE_TWS;   // A/B timing builds only
+    // fp64 C rows 10-24 % dense over >= 16384 columns: sparse tiles of 8192 columns (2048-slot
+    // windows; half the items, A-row reads and segment-table lookups of 4096-column tiles;
+    // config 5: 149.3 -> 124.8 ms per product)
+    if (B.value_type == SPG_R_64F && SPG_TILE_LEAN && SPG_SP_LEAN && tws == 12 && frac >= 0.1 &&
+        B.cols >= 16384 && frac * 8192.0 <= 0.95 * 2048)
+        tws = 13;
+    if (SPG_TILE_TWS >= 8 && SPG_TILE_TWS <= 14) tws = SPG_TILE_TWS;   // A/B timing builds only
     if (frac * (double)(1 << tws) < 64.0) return false;
     // the tile-major B's segment table is int32 and its records are addressed with 32-bit
     // byte offsets
@@ -939,10 +945,20 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
         };
         if constexpr (OrderedLdsAdd<T>::value) {
             if (!dense && SPG_TILE_LEAN && SPG_SP_LEAN) {   // sparse tiles, ordered LDS adds
-                hipExtLaunchKernelGGL((k_tile_sp<T, IP>), dim3(tile_grid(n * p.G, SP_WPB)), dim3(SP_WPB * WAVE), 0,
-                                      h->stream, kt.a, kt.b, 0, r0, n, p.tws, p.G, Ap, Aj, Ax, p.B.rows,
-                                      (const uint32_t*)p.brec, (const int32_t*)p.tptr, (const uint32_t*)p.bitmap,
-                                      (const int64_t*)tile_chunk_items(p, c), cj, cx, alpha, sent(2));   // (sparse tiles' region)
+                auto sp = [&](auto capc) {
+                    constexpr int CAP = decltype(capc)::value;
+                    hipExtLaunchKernelGGL((k_tile_sp<T, IP, CAP>), dim3(tile_grid(n * p.G, SP_WPB)), dim3(SP_WPB * WAVE),
+                                          0, h->stream, kt.a, kt.b, 0, r0, n, p.tws, p.G, Ap, Aj, Ax, p.B.rows,
+                                          (const uint32_t*)p.brec, (const int32_t*)p.tptr, (const uint32_t*)p.bitmap,
+                                          (const int64_t*)tile_chunk_items(p, c), cj, cx, alpha,
+                                          sent(2));   // (sparse tiles' region)
+                };
+                if constexpr (std::is_same<T, double>::value) {
+                    if (p.tws > 12) sp(std::integral_constant<int, 2048>{});
+                    else sp(std::integral_constant<int, 1024>{});
+                } else {
+                    sp(std::integral_constant<int, 1024>{});
+                }
                 SPG_LAUNCHED(h);
                 continue;
             }

@@ -380,9 +380,16 @@ __global__ __launch_bounds__(DN_WPB * WAVE) void k_tile_dn(
 // Output per window: the compact accumulator is already in C order, so the values leave with
 // coalesced stores; then every lane lists its bitmap words' columns (one per set bit) into the
 // freed accumulator, and the column indices leave the same way.
-template <typename T> struct SpLds {
-    T acc[TILE_CAP + WAVE];       // compact accumulator of one window; + lane-private slots
-    uint2 bw[TILE_NWMAX];         // (bitmap word, popcount prefix)
+// The kernel is instantiated for two tile widths: up to 4096 columns (1024-slot windows, 128
+// bitmap words) and, fp64 only, 8192 columns (2048-slot windows, 256 words: config 5's
+// shape, numeric 128.7 -> 103.9 ms; 16384 columns measured 143 ms).
+template <int CAP> struct SpGeom {
+    static constexpr int NWMAX = CAP / 8;          // bitmap words of the widest tile (TW = 4 * CAP)
+    static constexpr int WPL = NWMAX / WAVE;       // bitmap words per lane (at most)
+};
+template <typename T, int CAP> struct SpLds {
+    T acc[CAP + WAVE];            // compact accumulator of one window; + lane-private slots
+    uint2 bw[SpGeom<CAP>::NWMAX];   // (bitmap word, popcount prefix)
     DnEnt<T> ent[WAVE + 1];
     uint8_t mk[NUM_MK];
 #ifdef SPG_LDS_PAD
@@ -391,22 +398,24 @@ template <typename T> struct SpLds {
 };
 constexpr int SP_WPB = 1;   // 11.3 KB of LDS per wave: one-wave blocks pack a CU best
 
-template <typename T, typename IP>
-__global__ __launch_bounds__(SP_WPB * WAVE) __attribute__((amdgpu_waves_per_eu(sizeof(T) > 8 ? 2 : 4))) void k_tile_sp(
+template <typename T, typename IP, int SP_CAP>
+__global__ __launch_bounds__(SP_WPB * WAVE) __attribute__((amdgpu_waves_per_eu((sizeof(T) > 8 || SP_CAP > 1024) ? 2 : 4)))
+void k_tile_sp(
     int64_t row0, int64_t nrows, int tws, int G, const IP* __restrict__ Ap,
     const int32_t* __restrict__ Aj, const T* __restrict__ Ax, int64_t K,
     const uint32_t* __restrict__ brec, const int32_t* __restrict__ tptr, const uint32_t* __restrict__ bitmap,
     const int64_t* __restrict__ item_off, int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha, uint32_t sent) {
     static_assert(OrderedLdsAdd<T>::value, "ordered LDS add needed");
-    static_assert(sizeof(T) * (TILE_CAP + WAVE) >= 4 * TILE_CAP, "column list fits the accumulator");
+    static_assert(sizeof(T) * (SP_CAP + WAVE) >= 4 * SP_CAP, "column list fits the accumulator");
+    constexpr int SP_WPL = SpGeom<SP_CAP>::WPL;
     constexpr int NB = sizeof(T) > 8 ? 4 : 8;
-    __shared__ __attribute__((aligned(16))) SpLds<T> lds[SP_WPB];
+    __shared__ __attribute__((aligned(16))) SpLds<T, SP_CAP> lds[SP_WPB];
     const int l = lane_id();
     const int wv = uniform((int)(threadIdx.x >> 6));
-    SpLds<T>& S = lds[wv];
+    SpLds<T, SP_CAP>& S = lds[wv];
     const int TW = 1 << tws;
     const int nw = TW >> 5;                    // bitmap words of a tile
-    const int wpl = (nw + WAVE - 1) / WAVE;    // words per lane (<= 2)
+    const int wpl = (nw + WAVE - 1) / WAVE;    // words per lane (<= SP_WPL)
     const char* __restrict__ rb = reinterpret_cast<const char*>(brec);
     const uint32_t items = (uint32_t)(nrows * G);
     const bool one = alpha == (T)1;
@@ -421,10 +430,10 @@ __global__ __launch_bounds__(SP_WPB * WAVE) __attribute__((amdgpu_waves_per_eu(s
         // the item's bitmap (lane owns wpl words) and its popcount prefix
         const uint32_t* __restrict__ ibits = bitmap + item * nw;
         const int w0 = min(nw, l * wpl), w1 = min(nw, w0 + wpl);
-        uint32_t wd[2] = {0u, 0u};
+        uint32_t wd[SP_WPL] = {};
         int mine = 0;
 #pragma unroll
-        for (int q = 0; q < 2; ++q)
+        for (int q = 0; q < SP_WPL; ++q)
             if (w0 + q < w1) {
                 wd[q] = ibits[w0 + q];
                 mine += __popc(wd[q]);
@@ -455,7 +464,7 @@ __global__ __launch_bounds__(SP_WPB * WAVE) __attribute__((amdgpu_waves_per_eu(s
         {
             int run = p0;
 #pragma unroll
-            for (int q = 0; q < 2; ++q)
+            for (int q = 0; q < SP_WPL; ++q)
                 if (w0 + q < w1) {
                     S.bw[w0 + q] = make_uint2(wd[q], (uint32_t)run);
                     run += __popc(wd[q]);
@@ -463,11 +472,11 @@ __global__ __launch_bounds__(SP_WPB * WAVE) __attribute__((amdgpu_waves_per_eu(s
         }
         const int lo = g * TW;
         for (int L0 = 0; L0 < WAVE;) {
-            // window: lanes [L0, L1) whose words' entries fit TILE_CAP slots
+            // window: lanes [L0, L1) whose words' entries fit SP_CAP slots
             int L1 = WAVE, wb = 0, wn = nnz;
-            if (nnz > TILE_CAP) {
+            if (nnz > SP_CAP) {
                 wb = readlane_i(p0, L0);
-                L1 = (int)__popcll(__ballot(pincl <= wb + TILE_CAP));
+                L1 = (int)__popcll(__ballot(pincl <= wb + SP_CAP));
                 if (L1 <= L0) L1 = L0 + 1;
                 wn = (L1 < WAVE ? readlane_i(p0, L1) : nnz) - wb;
             }
@@ -477,7 +486,7 @@ __global__ __launch_bounds__(SP_WPB * WAVE) __attribute__((amdgpu_waves_per_eu(s
             if (L0 > 0) preload();   // (the walk consumes the queue; rare later windows reload it)
             dn_walk<T, NB>(&S, S.acc, l, tp, a0, nA, aq, sq, Aj, Ax, rb, sent,
                            [&](int rc) -> int {
-                               if (rc < clo || rc >= chi) return TILE_CAP + l;   // (sentinels too)
+                               if (rc < clo || rc >= chi) return SP_CAP + l;   // (sentinels too)
                                const uint2 b = S.bw[rc >> 5];
                                return (int)b.y + __popc(b.x & ((1u << (rc & 31)) - 1u)) - wb;
                            },
@@ -490,7 +499,7 @@ __global__ __launch_bounds__(SP_WPB * WAVE) __attribute__((amdgpu_waves_per_eu(s
                     for (int p0 = 0; p0 < wn; p0 += 4 * WAVE) {
                         T v[4];
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) v[e] = S.acc[min(p0 + e * WAVE + l, TILE_CAP + WAVE - 1)];
+                        for (int e = 0; e < 4; ++e) v[e] = S.acc[min(p0 + e * WAVE + l, SP_CAP + WAVE - 1)];
 #pragma unroll
                         for (int e = 0; e < 4; ++e) {
                             const int p = p0 + e * WAVE + l;
@@ -506,7 +515,7 @@ __global__ __launch_bounds__(SP_WPB * WAVE) __attribute__((amdgpu_waves_per_eu(s
                 if (l >= L0 && l < L1) {
                     int pos = p0 - wb;
 #pragma unroll
-                    for (int q = 0; q < 2; ++q) {
+                    for (int q = 0; q < SP_WPL; ++q) {
                         uint32_t w = wd[q];
                         const int cb = lo + 32 * (w0 + q);
                         while (w != 0u) {
@@ -520,7 +529,7 @@ __global__ __launch_bounds__(SP_WPB * WAVE) __attribute__((amdgpu_waves_per_eu(s
                 for (int p0 = 0; p0 < wn; p0 += 4 * WAVE) {
                     uint32_t v[4];
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) v[e] = cl[min(p0 + e * WAVE + l, TILE_CAP - 1)];
+                    for (int e = 0; e < 4; ++e) v[e] = cl[min(p0 + e * WAVE + l, SP_CAP - 1)];
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
                         const int p = p0 + e * WAVE + l;

@@ -102,7 +102,7 @@ def _check_structure(A, B, C, n, density, tile_width):
         assert bool(ok.all()), f"columns not increasing in rows [{r0}, {r1})"
         rid = torch.repeat_interleave(torch.arange(r1 - r0, device=cols.device), lens[r0:r1])
         items = torch.bincount(rid * G + (cols // tile_width).to(torch.int64), minlength=(r1 - r0) * G)
-        big = torch.nonzero(items.view(r1 - r0, G).max(dim=1).values > TILE_CAP).flatten() + r0
+        big = torch.nonzero(items.view(r1 - r0, G).max(dim=1).values > window_cap(tile_width)).flatten() + r0
         over_cap.append(big.cpu().numpy())
         del cols, start, ok, rid, items
     return int(P_i.sum()), lens.cpu().numpy(), np.concatenate(over_cap) if over_cap else np.zeros(0, np.int64)
@@ -111,11 +111,17 @@ def _check_structure(A, B, C, n, density, tile_width):
 TILE_CAP = 1024   # entries of one tile-item accumulator window (spgemm_tile.hpp)
 
 
+def window_cap(tile_width):
+    """Accumulator window of a sparse tile item: 2048 slots on 8192-column tiles
+    (k_tile_sp<double, .., 2048>), else TILE_CAP."""
+    return 2048 if tile_width == 8192 else TILE_CAP
+
+
 def _stratified_rows(A, C_lens, chunk_rows, over_cap, total=2048, seed=0):
     """Rows where the schedule changes, then uniform ones up to `total`:
     * the first and last row of every row chunk (ALG3's chunk cut) and their neighbours;
     * the longest A rows and the largest C rows;
-    * rows with a tile item past TILE_CAP entries (windowed items, sparse tiles);
+    * rows with a tile item past its accumulator window (windowed items, sparse tiles);
     * the first and last rows of the matrix."""
     m = A.shape[0]
     a_lens = (A.indptr[1:] - A.indptr[:-1]).cpu().numpy()

@@ -323,6 +323,33 @@ def test_tile_path_dense_2048(neg):
         _assert_same(_gpu(A, B, alg=alg, cf=cf), ref)
 
 
+def test_tile_path_sparse_8192():
+    """fp64 C rows 10-24 % dense over >= 16384 columns take 8192-column sparse tiles
+    (k_tile_sp<double, .., 2048>; config 5's shape): skewed A rows whose items need several
+    2048-slot windows, an empty A row, a ragged last tile, alpha != 1, every algorithm (ALG3
+    with many chunks).  plan_info confirms the width."""
+    from spmm_amd import cusparse
+    from spmm_amd.sparse import csr_matrix
+    rng = np.random.default_rng(34)
+    A = sp.random(300, 40000, density=0.0075, format="lil", random_state=rng)
+    for r in (0, 7, 151, 299):   # 3000-entry rows: ~35,800 C entries, several windows per item
+        A[r, :] = sp.random(1, 40000, density=0.075, format="lil", random_state=rng)
+    for r in range(3, 300, 37):
+        A[r, :] = 0
+    A = sp.csr_matrix(A)
+    B = sp.random(40000, 40000, density=0.00075, format="csr", random_state=rng)
+    for M in (A, B):
+        M.sum_duplicates()
+        M.sort_indices()
+    dA, dB = csr_matrix(A, device=_dev()), csr_matrix(B, device=_dev())
+    info = cusparse.plan_info(dA, dB, alg=2)
+    assert info["tile_width"] == 8192 and not info["dense_tiles"], info
+    ref = oracle.spgemm(A, B, alpha=0.5, keep_zeros=True, sort=True)
+    assert np.diff(ref[0]).max() > 2 * 2048 * 4   # dense rows: several windows per item
+    for alg, cf in [(1, 0.2), (2, 0.2), (3, 0.2), ("3c", 0.02)]:
+        _assert_same(_gpu(A, B, alg=alg, alpha=0.5, cf=cf), ref)
+
+
 def test_tile_path_dense_tiles_fp32_int64():
     """1024-column tiles over a dense C (batches of 64 A entries with > 1024 products per
     batch and tile), fp32 values, int64 row pointers, B with empty rows."""
