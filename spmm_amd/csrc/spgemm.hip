@@ -1308,23 +1308,26 @@ spg_status_t spg_plan(spg_handle_t h, const spg_csr_t* A, const spg_csr_t* B, sp
             tmp.chunk_nz = h->q_chunk_nz;
             tmp.seg_len = h->q_seg_len;
         } else {
-            if ((st = plan_chunks(h, tmp))) return st;
             // The ALG3 cap: chunk_fraction of the single-pass (ALG1) buffer, P entries of
             // C's (index, value) pairs -- the working set cuSPARSE's ALG3 trades time against
             // (estimateMemory, spgemm_from_txt_alg3.cu:195-202).  When the unchunked
-            // workspace is already within it, chunking would only add launches: one chunk.
+            // workspace is already within it, chunking would only add launches: one chunk,
+            // decided from P alone (one scalar read back), without the per-row product
+            // prefix and the row pointer the chunk cut needs on the host.
             spg_plan_s whole = tmp;
             whole.chunk_rows.assign({0, A->rows});
             whole.chunk_nz.assign({0, A->nnz});
-            whole.seg_len = A->nnz;
-            if (tmp.use_tile) whole.seg_len = 1;
-            const double cap = (double)chunk_fraction * (double)std::max<int64_t>(tmp.P, 0) *
-                               (double)(sizeof(int32_t) + vbytes(A->value_type));
+            whole.seg_len = tmp.use_tile ? 1 : A->nnz;
             // (SPG_ALG3_CHUNK_ALWAYS=1 keeps the chunks regardless: a schedule-only switch the
             // GPU tests use to cover the chunked paths on small inputs; results are identical)
             const char* ae = std::getenv("SPG_ALG3_CHUNK_ALWAYS");
             const bool always = ae && std::strcmp(ae, "1") == 0;
-            if (!always && tmp.chunk_rows.size() > 2 && (double)make_layout(whole).total <= cap) {
+            if ((st = products_total(h, *A, *B, &tmp.P))) return st;
+            const double cap = (double)chunk_fraction * (double)std::max<int64_t>(tmp.P, 0) *
+                               (double)(sizeof(int32_t) + vbytes(A->value_type));
+            if (always || (double)make_layout(whole).total > cap) {
+                if ((st = plan_chunks(h, tmp))) return st;
+            } else {
                 tmp.chunk_rows = whole.chunk_rows;
                 tmp.chunk_nz = whole.chunk_nz;
                 tmp.seg_len = whole.seg_len;
