@@ -254,13 +254,16 @@ spg_status_t spg_spgemm_ws(spg_handle_t handle, const spg_csr_t *A, const spg_cs
 typedef enum {
     SPG_PHASE_PRODUCTS = 0,   /* k_row_products: P_i per row                      */
     SPG_PHASE_SCAN = 1,       /* k_scan_lb / k_items_to_rowptr: prefix sums       */
-    SPG_PHASE_SYMBOLIC = 2,   /* k_short (count) / k_tile_sym / k_symbolic        */
-    SPG_PHASE_NUMERIC = 3,    /* k_short / k_tile / k_numeric: values (ALG1 also  */
-                              /* structure); one kernel per launch                */
+    SPG_PHASE_SYMBOLIC = 2,   /* k_row (count) / k_tile_sym(_seg) / k_symbolic     */
+    SPG_PHASE_NUMERIC = 3,    /* k_row / k_tile_dn / k_tile_sp / k_tile /          */
+                              /* k_numeric: values (ALG1 also structure); one       */
+                              /* kernel per launch                                  */
     SPG_PHASE_COMPACT = 4,    /* k_compact: ALG1 copy into C                        */
     SPG_PHASE_VALIDATE = 5,   /* k_validate                                         */
     SPG_PHASE_SPILL = 6,      /* k_symbolic / k_numeric over the rows the short-row */
-                              /* kernel handed on (list mode); k_tile_index         */
+                              /* kernel handed on (list mode); the tile path's      */
+                              /* once-per-plan builds (k_tile_index, k_bt_count,     */
+                              /* k_bj16, k_bt_pack)                                  */
     SPG_PHASE_SPMV = 7,       /* k_spmv                                             */
     SPG_NUM_PHASES = 8
 } spg_phase_t;
