@@ -60,8 +60,14 @@ def vs_table(path):
 
 
 if __name__ == "__main__":
-    d = sys.argv[1] if len(sys.argv) > 1 else "profiles/r02_sweeps"
+    # usage: reference_grid.py [dir with r02_*.txt] | [alg_comparison.txt [spgemm_vs_spmv.txt]]
+    arg = sys.argv[1] if len(sys.argv) > 1 else "profiles/r02_sweeps"
+    if arg.endswith(".txt"):
+        alg_file, vs_file = arg, (sys.argv[2] if len(sys.argv) > 2 else None)
+    else:
+        alg_file, vs_file = f"{arg}/r02_alg_comparison.txt", f"{arg}/r02_spgemm_vs_spmv.txt"
     print("### SpGEMM_alg_comparison grid (fp32, 100 runs, median; reference: BASELINE.md 1a, different hardware, context only)\n")
-    alg_table(f"{d}/r02_alg_comparison.txt")
-    print("\n### SpGEMM_vs_SpMV, SpGEMM half (A_csr @ B_csr; reference: BASELINE.md 1b, different hardware, context only)\n")
-    vs_table(f"{d}/r02_spgemm_vs_spmv.txt")
+    alg_table(alg_file)
+    if vs_file:
+        print("\n### SpGEMM_vs_SpMV, SpGEMM half (A_csr @ B_csr; reference: BASELINE.md 1b, different hardware, context only)\n")
+        vs_table(vs_file)
