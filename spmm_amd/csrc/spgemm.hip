@@ -173,6 +173,10 @@ inline bool row_kernel_enabled() {
 #define SPG_TILE_TWS 0
 #endif
 //   SPG_TILE_LEAN   0 keeps the owner-round k_tile on dense tiles (A/B against k_tile_dn)
+//   SPG_DN_PH       k phases per dense 2048-column item (k_tile_dn<.., PH>; 1 = unphased)
+#ifndef SPG_DN_PH
+#define SPG_DN_PH 1
+#endif
 #ifndef SPG_TILE_LEAN
 #define SPG_TILE_LEAN 1
 #endif
@@ -228,7 +232,8 @@ inline bool want_tile(const spg_csr_t& A, const spg_csr_t& B, int& tws, int& G) 
     if (B.value_type == SPG_R_64F && SPG_TILE_LEAN && SPG_SP_LEAN && tws == 12 && frac >= 0.1 &&
         B.cols >= 16384 && frac * 8192.0 <= 0.95 * 2048)
         tws = 13;
-    if (SPG_TILE_TWS >= 8 && SPG_TILE_TWS <= 14) tws = SPG_TILE_TWS;   // A/B timing builds only
+    // (A/B timing builds only; at most 8192 columns: k_tile_sp<.., 2048> holds 256 bitmap words)
+    if (SPG_TILE_TWS >= 8 && SPG_TILE_TWS <= 13) tws = SPG_TILE_TWS;
     if (frac * (double)(1 << tws) < 64.0) return false;
     // the tile-major B's segment table is int32 and its records are addressed with 32-bit
     // byte offsets
@@ -392,8 +397,10 @@ spg_status_t launch_scan(spg_handle_t h, int64_t n, const IN* in, OUT* out,
     const int64_t tiles = scan_tiles(n);
     if (zero_status)
         SPG_HIP(h, hipMemsetAsync(status, 0, sizeof(unsigned long long) * (size_t)(tiles + 1), h->stream));
+    // (the handle's wait bound: SPG_LB_SPIN_TICKS=0 sends every look-back of an out-of-place
+    // scan down its direct path, for the tests; in-place scans always wait, k_scan_lb)
     timed_launch(h, SPG_PHASE_SCAN, k_scan_lb<OUT, IN>, dim3((unsigned)tiles), dim3(BLOCK), n, in, out, status, scal,
-                 move_cnt, move_dst, host_mirror, mirror_gen, mirror_n, seed);
+                 move_cnt, move_dst, host_mirror, mirror_gen, mirror_n, seed, h->lb_spin);
     SPG_LAUNCHED(h);
     return SPG_STATUS_SUCCESS;
 }
@@ -965,7 +972,13 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
             if (dense && SPG_TILE_LEAN) {   // ordered LDS adds (spgemm_tile_dn.hpp)
                 auto dn = [&](auto twd) {
                     constexpr int TWD = decltype(twd)::value;
-                    hipExtLaunchKernelGGL((k_tile_dn<T, IP, TWD>), dim3(tile_grid(n * p.G, DN_WPB)), dim3(DN_WPB * WAVE),
+                    // k-phased items (SPG_DN_PH, A/B builds; fp64 2048-column tiles)
+                    constexpr int PH = (std::is_same<T, double>::value && TWD == 2048) ? SPG_DN_PH : 1;
+                    constexpr int W = dn_wpb<PH>();
+                    // (phased: one 8-wave block per CU, persistent, so a CU's items stay in step)
+                    const unsigned grid = PH > 1 ? std::min<unsigned>(tile_grid(n * p.G, W), (unsigned)(h->cus + 7) / 8 * 8)
+                                                 : tile_grid(n * p.G, W);
+                    hipExtLaunchKernelGGL((k_tile_dn<T, IP, TWD, PH>), dim3(grid), dim3(W * WAVE),
                                           0, h->stream, kt.a, kt.b, 0, r0, n, p.tws, p.G, Ap, Aj, Ax, p.B.rows,
                                           (const uint32_t*)p.brec, (const int32_t*)p.tptr,
                                           (const int64_t*)tile_chunk_items(p, c), cj, cx, alpha,

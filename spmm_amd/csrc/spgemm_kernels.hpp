@@ -907,13 +907,18 @@ __global__ __launch_bounds__(BLOCK) void k_scan_lb(int64_t n, const IN* in, OUT*
                                                    int64_t* __restrict__ move_dst = nullptr,
                                                    int64_t* __restrict__ host_mirror = nullptr,
                                                    int64_t mirror_gen = 0, int mirror_n = 0,
-                                                   const int64_t* seed = nullptr) {
+                                                   const int64_t* seed = nullptr, uint64_t spin = SCAN_SPIN) {
     __shared__ ScanLds L;
     __shared__ int bid_s;
     if (threadIdx.x == 0) bid_s = (int)atomicAdd(&status[0], 1ull);
     __syncthreads();
+    // An in-place scan (the tile path's segment table and item counts) must not take the
+    // bounded wait's direct-sum fallback: earlier tiles have already replaced their inputs
+    // with exclusive prefixes, so in[0 .. base) no longer holds the counts.  Its
+    // waits stay unbounded; the ticket order guarantees every predecessor has started.
+    const bool in_place = reinterpret_cast<const void*>(in) == reinterpret_cast<const void*>(out);
     scan_tile<OUT, IN>(bid_s, n, in, out, status + 1, scalars, move_cnt, move_dst, host_mirror, mirror_gen,
-                       mirror_n, seed, L);
+                       mirror_n, seed, L, nullptr, in_place ? ~0ull : spin);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -138,11 +138,15 @@ __device__ __forceinline__ void dn_group_markers(uint8_t* mk, int l, int cnt, in
 // markers; per U chunks the lane -> entry max-scans, one 16-byte table read and one record load
 // per chunk (all in flight), then per chunk in order one multiply and one ds_add_f64 into
 // acc[slot(column)] and hit(slot).  `sent` is the byte offset of the kernel's sentinel region.
-template <typename T, int NB, typename L, typename Slot, typename Hit>
+// KR (k-phased items, k_tile_dn<.., PH > 1>): only the A entries whose column k lies in
+// [klo, khi) contribute (`kq` carries the preloaded batches' columns); the entries are sorted, so
+// a phase is a contiguous run of them and batches wholly outside it are skipped.
+template <typename T, int NB, bool KR = false, typename L, typename Slot, typename Hit>
 __device__ __forceinline__ void dn_walk(L* lp, T* acc, int l, const int32_t* __restrict__ tp, int64_t a0, int nA,
                                         T (&aq)[NB], uint2 (&sq)[NB], const int32_t* __restrict__ Aj,
                                         const T* __restrict__ Ax, const char* __restrict__ rb, uint32_t sent,
-                                        Slot&& slot, Hit&& hit) {
+                                        Slot&& slot, Hit&& hit, int32_t (*kq)[NB] = nullptr, int klo = 0,
+                                        int khi = 0) {
     constexpr int U = sizeof(T) > 8 ? 4 : 8;     // chunks in flight
     constexpr uint32_t RB = 4u * (uint32_t)rec_words<T>();   // bytes of one B record
     DnEnt<T>* ent = lp->ent;
@@ -157,16 +161,27 @@ __device__ __forceinline__ void dn_walk(L* lp, T* acc, int l, const int32_t* __r
             cnt = (int)(sq[0].y - sq[0].x);
             beg = sq[0].x;
             av = aq[0];
+            if constexpr (KR) {
+                if ((*kq)[0] < klo || (*kq)[0] >= khi) cnt = 0;
+#pragma unroll
+                for (int q = 0; q + 1 < NB; ++q) (*kq)[q] = (*kq)[q + 1];
+            }
 #pragma unroll
             for (int q = 0; q + 1 < NB; ++q) {
                 sq[q] = sq[q + 1];
                 aq[q] = aq[q + 1];
             }
         } else if (b + l < nA) {
-            const uint2 se = seg_pair(tp, Aj[a0 + b + l]);
-            cnt = (int)(se.y - se.x);
-            beg = se.x;
-            av = Ax[a0 + b + l];
+            const int32_t k = Aj[a0 + b + l];
+            if (!KR || (k >= klo && k < khi)) {
+                const uint2 se = seg_pair(tp, k);
+                cnt = (int)(se.y - se.x);
+                beg = se.x;
+                av = Ax[a0 + b + l];
+            }
+        }
+        if constexpr (KR) {
+            if (!__ballot(cnt != 0)) continue;   // (a batch outside the phase)
         }
         const int incl = wave_incl_sum_dpp(cnt);
         const int off = incl - cnt;
@@ -244,33 +259,14 @@ __device__ __forceinline__ void dn_walk(L* lp, T* acc, int l, const int32_t* __r
     }
 }
 
-// One dense-tile item (row, tile g of TW <= 1024 columns) on one wave: clear the accumulator,
-// the ordered product walk with slot = column, then the output 64 columns at a time from hit[]
-// or (dn_sent) the slots that left -0.0 (ballot + lane rank give positions), straight to C.
-template <typename T, int NB, int TWD>
-__device__ __forceinline__ void dn_item(DnLds<T, TWD>& S, int l, int TW, int lo, int nnz, const int32_t* __restrict__ tp,
-                                        int64_t a0, int nA, T (&aq)[NB], uint2 (&sq)[NB],
-                                        const int32_t* __restrict__ Aj,
-                                        const T* __restrict__ Ax, const char* __restrict__ rb, uint32_t sent,
-                                        int32_t* __restrict__ crow,
+// The item's output: its structure 64 columns at a time from hit[] or (dn_sent) the slots that
+// left -0.0 (ballot + lane rank give positions), straight to C; the rare -0.0 re-walk.
+template <typename T, int TWD>
+__device__ __forceinline__ void dn_emit(DnLds<T, TWD>& S, int l, int TW, int lo, int nnz, const int32_t* __restrict__ tp,
+                                        int64_t a0, int nA, const int32_t* __restrict__ Aj,
+                                        const char* __restrict__ rb, int32_t* __restrict__ crow,
                                         T* __restrict__ xrow, T alpha) {
     constexpr uint32_t RB = 4u * (uint32_t)rec_words<T>();
-    wsync();
-    {   // clear the accumulator (-0.0: dn_sent) and the hit bytes (16-byte stores; TW is a
-        // multiple of 64)
-        uint4* a4 = reinterpret_cast<uint4*>(S.acc);
-        const uint32_t hi = dn_sent<T>() ? 0x80000000u : 0u;       // -0.0's sign bit
-        const uint32_t lw = sizeof(T) == 4 ? hi : 0u;              // (fp32: every word is a value)
-        for (int q = l; q < TW * (int)sizeof(T) / 16; q += WAVE) a4[q] = make_uint4(lw, hi, lw, hi);
-        if constexpr (!dn_sent<T>()) {
-            uint4* h4 = reinterpret_cast<uint4*>(S.hit);
-            for (int q = l; q < TW / 16; q += WAVE) h4[q] = make_uint4(0u, 0u, 0u, 0u);
-        }
-    }
-    dn_walk<T, NB>(&S, S.acc, l, tp, a0, nA, aq, sq, Aj, Ax, rb, sent, [&](int c) { return c; },
-                   [&](int c) {
-                       if constexpr (!dn_sent<T>()) S.hit[c] = 1;
-                   });
     wsync();
     // the item's structure, 64 columns at a time: hit[] or (dn_sent) the non -0.0 slots
     // (4 column groups per round: their LDS reads in flight together, TW >= 256)
@@ -324,38 +320,91 @@ __device__ __forceinline__ void dn_item(DnLds<T, TWD>& S, int l, int TW, int lo,
     }
 }
 
+// clear an item's accumulator
+template <typename T, int TWD>
+__device__ __forceinline__ void dn_clear(DnLds<T, TWD>& S, int l, int TW) {
+    wsync();
+    // clear the accumulator (-0.0: dn_sent) and the hit bytes (16-byte stores; TW is a
+    // multiple of 64)
+    uint4* a4 = reinterpret_cast<uint4*>(S.acc);
+    const uint32_t hi = dn_sent<T>() ? 0x80000000u : 0u;       // -0.0's sign bit
+    const uint32_t lw = sizeof(T) == 4 ? hi : 0u;              // (fp32: every word is a value)
+    for (int q = l; q < TW * (int)sizeof(T) / 16; q += WAVE) a4[q] = make_uint4(lw, hi, lw, hi);
+    if constexpr (!dn_sent<T>()) {
+        uint4* h4 = reinterpret_cast<uint4*>(S.hit);
+        for (int q = l; q < TW / 16; q += WAVE) h4[q] = make_uint4(0u, 0u, 0u, 0u);
+    }
+}
+
+// One dense-tile item (row, tile g of TW <= TWD columns) on one wave: clear the accumulator,
+// the ordered product walk with slot = column, then the output.
+template <typename T, int NB, int TWD>
+__device__ __forceinline__ void dn_item(DnLds<T, TWD>& S, int l, int TW, int lo, int nnz, const int32_t* __restrict__ tp,
+                                        int64_t a0, int nA, T (&aq)[NB], uint2 (&sq)[NB],
+                                        const int32_t* __restrict__ Aj,
+                                        const T* __restrict__ Ax, const char* __restrict__ rb, uint32_t sent,
+                                        int32_t* __restrict__ crow,
+                                        T* __restrict__ xrow, T alpha) {
+    dn_clear(S, l, TW);
+    dn_walk<T, NB>(&S, S.acc, l, tp, a0, nA, aq, sq, Aj, Ax, rb, sent, [&](int c) { return c; },
+                   [&](int c) {
+                       if constexpr (!dn_sent<T>()) S.hit[c] = 1;
+                   });
+    dn_emit<T, TWD>(S, l, TW, lo, nnz, tp, a0, nA, Aj, rb, crow, xrow, alpha);
+}
 // Numeric pass on dense tiles: one wave per (row, tile) item, items tile-major over the
 // XCD-aware block map (an XCD works through one tile at a time, so the tile's B slice and
 // segment table stay in its L2), the first NB batches' A entries and tile segments loaded up
 // front.
-template <typename T, typename IP, int TWD>
-__global__ __launch_bounds__(DN_WPB * WAVE) void k_tile_dn(
+//
+// PH > 1 (k-phased items, 8-wave blocks: one block per CU): every item walks its A entries in
+// PH phases of B rows, k in [ph*K/PH, (ph+1)*K/PH), and the block's waves meet at a barrier
+// after every phase.  The wave's accumulator carries the item across its phases and the
+// entries stay in (jj, kk) order inside and across phases, so the sums are exactly those of
+// PH = 1.  What changes is locality: a CU's waves gather from one 1/PH part of the tile's B
+// slice at a time (config 4's 2048-column slice is 8 MB against the XCD's 4 MB L2; at
+// 1/4 of it the gathers hit L2, abtest/gather_probe).
+template <int PH> constexpr int dn_wpb() { return PH > 1 ? 8 : DN_WPB; }
+template <typename T, typename IP, int TWD, int PH = 1>
+__global__ __launch_bounds__(dn_wpb<PH>() * WAVE) void k_tile_dn(
     int64_t row0, int64_t nrows, int tws, int G, const IP* __restrict__ Ap,
     const int32_t* __restrict__ Aj, const T* __restrict__ Ax, int64_t K,
     const uint32_t* __restrict__ brec, const int32_t* __restrict__ tptr,
     const int64_t* __restrict__ item_off, int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha, uint32_t sent) {
     static_assert(OrderedLdsAdd<T>::value, "ordered LDS add needed");
     constexpr int NB = sizeof(T) > 8 ? 4 : 8;    // A batches preloaded per item
-    __shared__ __attribute__((aligned(16))) DnLds<T, TWD> lds[DN_WPB];
+    constexpr int WPB = dn_wpb<PH>();
+    __shared__ __attribute__((aligned(16))) DnLds<T, TWD> lds[WPB];
     const int l = lane_id();
     const int wv = uniform((int)(threadIdx.x >> 6));
     DnLds<T, TWD>& S = lds[wv];
     const int TW = 1 << tws;
     const char* __restrict__ rb = reinterpret_cast<const char*>(brec);
     const uint32_t items = (uint32_t)(nrows * G);   // host keeps rows*G < 2^31
-    for (uint32_t it = xcd_block(gridDim.x) * DN_WPB + wv; it < items; it += gridDim.x * DN_WPB) {
-        const int g = (int)(it / (uint32_t)nrows);
-        const int64_t row = row0 + (int64_t)(it - (uint32_t)g * (uint32_t)nrows);
-        const int64_t item = (row - row0) * G + g;
-        const int64_t obase = ld_a(item_off + item);
-        const int nnz = (int)(ld_a(item_off + item + 1) - obase);
-        if (nnz == 0) continue;                      // (no product reaches this tile)
+    // (base is block-uniform: with PH > 1 every wave of the block meets every barrier, items
+    // or not)
+    for (uint32_t base = xcd_block(gridDim.x) * WPB; base < items; base += gridDim.x * WPB) {
+        const uint32_t it = base + wv;
+        bool live = it < items;
+        int g = 0, nnz = 0, nA = 0;
+        int64_t row = 0, obase = 0, a0 = 0;
+        if (live) {
+            g = (int)(it / (uint32_t)nrows);
+            row = row0 + (int64_t)(it - (uint32_t)g * (uint32_t)nrows);
+            const int64_t item = (row - row0) * G + g;
+            obase = ld_a(item_off + item);
+            nnz = (int)(ld_a(item_off + item + 1) - obase);
+            live = nnz > 0;                          // (no product reaches this tile)
+        }
+        if (PH == 1 && !live) continue;
         const int32_t* __restrict__ tp = tptr + (int64_t)g * (K + 1);
-        const int64_t a0 = Ap[row];
-        const int nA = (int)(Ap[row + 1] - a0);
         int32_t kq[NB];
         T aq[NB];
         uint2 sq[NB];
+        if (live) {
+            a0 = Ap[row];
+            nA = (int)(Ap[row + 1] - a0);
+        }
 #pragma unroll
         for (int q = 0; q < NB; ++q) {
             kq[q] = -1;
@@ -367,7 +416,34 @@ __global__ __launch_bounds__(DN_WPB * WAVE) void k_tile_dn(
         }
 #pragma unroll
         for (int q = 0; q < NB; ++q) sq[q] = kq[q] >= 0 ? seg_pair(tp, kq[q]) : make_uint2(0u, 0u);
-        dn_item<T, NB, TWD>(S, l, TW, g * TW, nnz, tp, a0, nA, aq, sq, Aj, Ax, rb, sent, Cj + obase, Cx + obase, alpha);
+        if constexpr (PH == 1) {
+            dn_item<T, NB, TWD>(S, l, TW, g * TW, nnz, tp, a0, nA, aq, sq, Aj, Ax, rb, sent, Cj + obase, Cx + obase,
+                                alpha);
+        } else {
+            if (live) dn_clear(S, l, TW);
+            for (int ph = 0; ph < PH; ++ph) {
+                if (live) {
+                    const int klo = (int)(K * ph / PH), khi = (int)(K * (ph + 1) / PH);
+                    int32_t kc[NB];
+                    T ac[NB];
+                    uint2 sc[NB];
+#pragma unroll
+                    for (int q = 0; q < NB; ++q) {
+                        kc[q] = kq[q];
+                        ac[q] = aq[q];
+                        sc[q] = sq[q];
+                    }
+                    dn_walk<T, NB, true>(&S, S.acc, l, tp, a0, nA, ac, sc, Aj, Ax, rb, sent,
+                                         [&](int c) { return c; },
+                                         [&](int c) {
+                                             if constexpr (!dn_sent<T>()) S.hit[c] = 1;
+                                         },
+                                         &kc, klo, khi);
+                }
+                __syncthreads();
+            }
+            if (live) dn_emit<T, TWD>(S, l, TW, g * TW, nnz, tp, a0, nA, Aj, rb, Cj + obase, Cx + obase, alpha);
+        }
     }
 }
 
