@@ -7,9 +7,15 @@ plan, symbolic with its nnz(C) host sync, C allocation, numeric), inputs residen
 Workloads (``--config``; ``auto`` = 4 at every N):
 
 * ``4`` (the N=1 headline: the largest single-GPU configuration of BASELINE.json, configs[3]):
-  N = 65536, density 5e-3, fp64, ALG3 chunked (chunk_fraction 0.2) -- the reference's ALG3
-  path, estimateMemory then a chunked compute (cupy_cusparse/spgemm_from_txt_alg3.cu:194-208).
-  nnz(C) = 3.46e9: int64 row pointer.  Inputs generated on the device (spmm_amd.gen.random_csr).
+  N = 65536, density 5e-3, fp64, ALG3 at chunk_fraction 0.2 -- the reference's ALG3 path,
+  estimateMemory then the compute (cupy_cusparse/spgemm_from_txt_alg3.cu:194-208).  The plan
+  chunks only when the unchunked workspace exceeds the cap (chunk_fraction x P entries of C);
+  config 4's dense tiles keep 0.35 GB of workspace against a 17 GB cap, so it runs ONE chunk
+  and the line says so (``config.n_chunks``, ``config.alg3_cap``).  The chunked schedule's cost
+  at scale is the ``alg3_chunked`` key: config 5 under ALG2 and under ALG3 at chunk_fraction
+  0.02 (>= 50 chunks), time and peak side by side (the reference's time / peak trade,
+  BASELINE.md 1a).  nnz(C) = 3.46e9: int64 row pointer.  Inputs generated on the device
+  (spmm_amd.gen.random_csr).
   At N > 1 it scales WEAK: rank r owns rows [r*65536, (r+1)*65536) of an (N*65536) x 65536
   A of the same density (rank 0's block is the N=1 A), B (258 MB) is broadcast from rank 0
   over RCCL/xGMI inside every step -- structure first, values in flight while the symbolic
@@ -60,7 +66,7 @@ CONFIGS = {
     "2": dict(n=16384, density=1e-3, alg=1, gen="scipy", steps=200, warmup=20,
               name="BASELINE config 2 (configs[1])"),
     "4": dict(n=65536, density=5e-3, alg=3, gen="device", steps=5, warmup=2,
-              name="BASELINE config 4 (configs[3], ALG3 chunked, HBM-capped)"),
+              name="BASELINE config 4 (configs[3], ALG3 with its HBM cap)"),
     "5": dict(n=262144, density=1e-3, alg=2, gen="device", steps=5, warmup=2,
               name="BASELINE config 5 (configs[4], row blocks, B broadcast)"),
 }
@@ -81,6 +87,7 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="budget of the CPU-baseline sample (0 disables it)")
     ap.add_argument("--no-config2", action="store_true", help="N=1: skip the config2 key")
+    ap.add_argument("--no-alg3-chunked", action="store_true", help="N=1: skip the alg3_chunked key")
     ap.add_argument("--config5-n", type=int, default=262144,
                     help="N>1: size of the strong-scaled config5 key (0 skips it)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
@@ -335,14 +342,22 @@ def load_hook(spec):
 
 
 def tile_kernel(ctx, A, B, alg, cf):
-    """Name of the numeric tile kernel the product runs (dense or sparse tiles)."""
+    """(name of the numeric tile kernel the product runs, its number of row chunks)."""
     if not ctx.gpu or B is None:
-        return "k_tile"
+        return "k_tile", 1
     from spmm_amd import cusparse
     info = cusparse.plan_info(A, B, alg=alg, chunk_fraction=cf)
+    nch = len(info["chunk_rows"]) - 1
     if info["path"] != "tile":
-        return info["path"]
-    return ("k_tile_dn" if info["dense_tiles"] else "k_tile_sp") + f" (TW={info['tile_width']}, {len(info['chunk_rows']) - 1} chunk(s))"
+        return info["path"], nch
+    return ("k_tile_dn" if info["dense_tiles"] else "k_tile_sp") + f" (TW={info['tile_width']}, {nch} chunk(s))", nch
+
+
+def alg3_label(alg, nch):
+    if alg != 3:
+        return f"ALG{alg}"
+    return (f"ALG3, {nch} chunks (cap binding)" if nch > 1
+            else "ALG3, 1 chunk (cap not binding: the unchunked workspace is within chunk_fraction x P entries)")
 
 
 def gen_device(ctx, n, dens, seed, tdt, rows=None, row_offset=0):
@@ -395,8 +410,9 @@ def run_config4(ctx, args, cfg, tdt, vb, hook):
     bid, sid = lib_ids(ctx)
     key = f"c4_n{n}_d{dens:g}_{args.dtype}_alg{alg}_w1"   # per-rank work = the N=1 product
     traffic, tb = traffic_for(args.pmc, key, bid, sid) if ctx.gpu else (None, None)
-    rf = roofline(ph, reps, tile_kernel(ctx, A, B, alg, cf),
-                  compulsory_bytes(A.shape[0], n, A.nnz, nnzB, nnzC, vb, ib_c), ms, traffic, tb, step_frac=(w == 1))
+    kname, nch = tile_kernel(ctx, A, B, alg, cf)
+    rf = roofline(ph, reps, kname, compulsory_bytes(A.shape[0], n, A.nnz, nnzB, nnzC, vb, ib_c), ms, traffic, tb,
+                  step_frac=(w == 1))
     cpu = None
     if r == 0 and w == 1 and args.cpu_seconds > 0 and ctx.gpu:
         A_h, B_h = A.get(), B.get()
@@ -404,7 +420,7 @@ def run_config4(ctx, args, cfg, tdt, vb, hook):
         cpu = cpu_baseline(A_h, B_h, sample, args.cpu_seconds)
     desc = (f"{cfg['name']}: random CSR {n}x{n} density={dens:g} {args.dtype} "
             f"(spmm_amd.gen.random_csr on the device, seeds {args.seed}/{args.seed + 1}), "
-            f"ALG{alg} chunked, chunk_fraction {cf}")
+            f"{alg3_label(alg, nch)}, chunk_fraction {cf}")
     if w > 1:
         desc += (f"; weak scaling: rank r owns rows [r*{n}, (r+1)*{n}) of a {w * n}x{n} A "
                  "(rank 0's block is the N=1 A), B broadcast over RCCL inside every step, no reduction")
@@ -412,7 +428,9 @@ def run_config4(ctx, args, cfg, tdt, vb, hook):
         "value": round(2.0 * P_all * steps / elapsed / 1e9, 3), "steps": steps, "warmup": warmup,
         "ms_per_step": round(ms, 5), "scaling": "weak",
         "config": {"workload": desc, "N": n, "rows_per_rank": n, "density": dens, "alg": alg,
-                   "chunk_fraction": cf, "nnzB": int(nnzB), "nnzA_rank0" if w > 1 else "nnzA": int(A.nnz),
+                   "chunk_fraction": cf, "n_chunks": nch,
+                   "alg3_cap": None if alg != 3 else ("binding" if nch > 1 else "not binding"),
+                   "nnzB": int(nnzB), "nnzA_rank0" if w > 1 else "nnzA": int(A.nnz),
                    "nnzC": int(nnz_all), "num_products": int(P_all),
                    "parallelism": "single GPU" if w == 1 else f"row-block x{w} (weak), B broadcast over RCCL"},
         "peak_hbm_bytes": int(peak_max), "roofline": rf,
@@ -487,16 +505,61 @@ def run_config5(ctx, args, cfg, n, tdt, vb, hook, steps, warmup):
     ms = elapsed / steps * 1e3
     reps = 1
     ph = phase_times(ctx, step, reps)
-    rf = roofline(ph, reps, tile_kernel(ctx, A, B, alg, cf), compulsory_bytes(A.shape[0], n, A.nnz, nnzB, nnzC, vb, ib_c),
+    kname, nch = tile_kernel(ctx, A, B, alg, cf)
+    rf = roofline(ph, reps, kname, compulsory_bytes(A.shape[0], n, A.nnz, nnzB, nnzC, vb, ib_c),
                   ms, None, None, step_frac=False)
     out = {"gflops": round(2.0 * P_all * steps / elapsed / 1e9, 3), "ms_per_step": round(ms, 5),
            "steps": steps, "warmup": warmup, "scaling": "strong", "N": n, "density": dens, "alg": alg,
-           "num_products": int(P_all), "nnzC": int(nnz_all), "rows_rank0": list(rows),
+           "num_products": int(P_all), "nnzC": int(nnz_all), "rows_rank0": list(rows), "n_chunks": nch,
            "peak_hbm_bytes_max_rank": int(peak_max), "b_broadcast_ms": None if bcast_ms is None else round(bcast_ms, 3),
            "roofline_rank0": rf, "phases_ms_per_step": {k: round(v[0] / reps, 5) for k, v in ph.items() if v[1]},
            "workload": (f"{cfg['name']}: random CSR {n}x{n} density={dens:g} {args.dtype}, ALG{alg}; "
                         f"{w} row blocks cut on the product prefix (each rank draws its own block), "
+                        f"{alg3_label(alg, nch)}, "
                         "B broadcast over RCCL inside every step")}
+    del A, B
+    return out
+
+
+def _device_sig(torch, x, piece=1 << 27):
+    """Position-weighted wrapping int64 sum of a 1-D integer tensor, computed in pieces."""
+    acc = torch.zeros((), dtype=torch.int64, device=x.device)
+    for s in range(0, x.numel(), piece):
+        v = x[s:s + piece].to(torch.int64)
+        w = torch.arange(s, s + v.numel(), device=x.device, dtype=torch.int64) % 1000003 + 1
+        acc += torch.sum(v * w)
+    return int(acc)
+
+
+def run_alg3_chunked(ctx, args, tdt, n=262144, dens=1e-3, cf=0.02, steps=2, warmup=1):
+    """ALG3's time / peak trade where its cap binds: config 5 on one GPU under ALG2
+    and under ALG3 at chunk_fraction `cf` (>= 50 equal-product row chunks), same inputs, the
+    results compared bit for bit on device (row pointer, columns, value bits)."""
+    from spmm_amd import cusparse
+    A = gen_device(ctx, n, dens, args.seed, tdt)
+    B = gen_device(ctx, n, dens, args.seed + 1, tdt)
+    P = cusparse.num_products(A, B)
+    out = {"N": n, "density": dens, "num_products": int(P),
+           "workload": f"BASELINE config 5 shape (N={n}, density {dens:g}) on one GPU: ALG2 vs ALG3 at chunk_fraction {cf}"}
+    ref = None
+    for alg, c in ((2, 0.2), (3, cf)):
+        elapsed, C = timed(ctx, lambda: cusparse.spgemm(A, B, alg=alg, chunk_fraction=c), steps, warmup)
+        _, nch = tile_kernel(ctx, A, B, alg, c)
+        key = "alg2" if alg == 2 else "alg3"
+        out[key] = {"chunk_fraction": c, "n_chunks": nch, "ms_per_step": round(elapsed / steps * 1e3, 3),
+                    "gflops": round(2.0 * P * steps / elapsed / 1e9, 3),
+                    "peak_hbm_bytes": int(cusparse.last_stats.peak_bytes)}
+        # the same C under both schedules: position-weighted sums of the arrays on the device,
+        # in pieces (no 190 GB copy to the host, no int64 copy of all of C)
+        torch = ctx.torch
+        sig = (_device_sig(torch, C.indptr.to(torch.int64)), _device_sig(torch, C.indices),
+               _device_sig(torch, C.data.view(torch.int64)))
+        ref = sig if ref is None else ref
+        out[key]["same_result_as_alg2"] = sig == ref
+        del C
+        torch.cuda.empty_cache()
+    out["alg3_over_alg2_time"] = round(out["alg3"]["ms_per_step"] / out["alg2"]["ms_per_step"], 3)
+    out["alg3_over_alg2_peak"] = round(out["alg3"]["peak_hbm_bytes"] / out["alg2"]["peak_hbm_bytes"], 3)
     del A, B
     return out
 
@@ -565,6 +628,8 @@ def main(argv=None):
         line.update(res)
         if ctx.world == 1 and ctx.gpu and not args.no_config2:
             line["config2"] = run_config2(ctx, args, CONFIGS["2"], npdt, vb, with_cpu=False)
+        if ctx.world == 1 and ctx.gpu and not args.no_alg3_chunked:
+            line["alg3_chunked"] = run_alg3_chunked(ctx, args, tdt)
         if ctx.world > 1 and args.config5_n > 0:
             line["config5"] = run_config5(ctx, args, CONFIGS["5"], args.config5_n, tdt, vb, hook,
                                           steps=3, warmup=1)
@@ -582,7 +647,7 @@ def main(argv=None):
                      "ms_per_step": res.pop("ms_per_step"), "scaling": "weak",
                      "peak_hbm_bytes": res.pop("peak_hbm_bytes"), "roofline": res.pop("roofline"),
                      "cpu_baseline": res.pop("cpu_baseline", None), "config": res})
-    line["lib_build_id"] = lib_ids(ctx)[0]
+    line["lib_build_id"], line["lib_source_id"] = lib_ids(ctx)
     if ctx.rank == 0:
         print(json.dumps(line), flush=True)
     if ctx.world > 1:

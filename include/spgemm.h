@@ -213,13 +213,17 @@ spg_status_t spg_validate_csr(spg_handle_t handle, const spg_csr_t *M, int *is_c
  * 2 tile path (tile_width columns per numeric tile, tiles_per_row tiles, dense_tiles 1
  * when the accumulator is addressed by column).  n_chunks row chunks (ALG3: the chunk
  * cut; otherwise 1); their n_chunks + 1 row boundaries go to chunk_rows (at most
- * `capacity` entries written; chunk_rows may be NULL when capacity is 0). */
+ * `capacity` entries written; chunk_rows may be NULL when capacity is 0).  lds_ordered 1
+ * when fp64 / complex128 tiles run the ordered-LDS-add kernels -- the handle's device check at
+ * spg_create found the ordering they rely on -- and 0 when they fall back to owner rounds
+ * (same results). */
 typedef struct {
     int path;
     int tile_width;
     int64_t tiles_per_row;
     int dense_tiles;
     int64_t n_chunks;
+    int lds_ordered;
 } spg_plan_info_t;
 spg_status_t spg_plan_info(spg_plan_t plan, spg_plan_info_t *info, int64_t *chunk_rows, int64_t capacity);
 

@@ -61,7 +61,7 @@ class SpgCsr(ctypes.Structure):
 class SpgPlanInfo(ctypes.Structure):
     """spg_plan_info_t"""
     _fields_ = [("path", ctypes.c_int), ("tile_width", ctypes.c_int), ("tiles_per_row", ctypes.c_int64),
-                ("dense_tiles", ctypes.c_int), ("n_chunks", ctypes.c_int64)]
+                ("dense_tiles", ctypes.c_int), ("n_chunks", ctypes.c_int64), ("lds_ordered", ctypes.c_int)]
 
 
 class SpgTiming(ctypes.Structure):

@@ -41,6 +41,11 @@ struct spg_handle_s {
     // (read once per handle) lowers it -- 0 sends every wait to that path, which the GPU
     // tests use to check it bit for bit; it cannot change any result.
     uint64_t lb_spin = SCAN_SPIN;
+    // the ordered-LDS property k_tile_dn / k_tile_sp rely on (same-address lanes of one
+    // ds_add_f64 apply in ascending lane order, DS ops in issue order), checked on the device
+    // at spg_create (lds_order_check); false sends fp64 tiles to k_tile's owner rounds, which
+    // need neither.  SPG_LDS_ORDERED=0 forces false (a schedule-only switch, for the tests).
+    bool lds_ordered = true;
     void* scratch = nullptr;        // internal device scratch (plan-time analysis)
     size_t scratch_bytes = 0;
     // per-phase timing (spg_set_timing / spg_get_timing)
@@ -82,6 +87,7 @@ struct spg_plan_s {
     bool use_short = false;         // dispatch the short-row kernel first
     bool use_row = true;            // short rows: k_row (false: the owner-round k_short)
     bool use_tile = false;          // wide-row path: (row, column tile) items
+    bool lean = true;               // fp64 tiles may use the ordered-LDS kernels (k_tile_dn / k_tile_sp)
     int tws = 10;                   // log2 of the tile width
     int G = 1;                      // tiles per row
     int TR = 1;                     // tiles per wave task (a run of one row's tiles)
@@ -211,7 +217,9 @@ inline bool want_short(const spg_csr_t& A, const spg_csr_t& B) {
 // Wide rows go to the tile path when their C rows are dense enough that a tile of up to
 // 4096 columns holds a useful number of entries.  The tile width keeps the expected
 // entries of a tile within TILE_CAP (or is at most TILE_CAP, which bounds them).
-inline bool want_tile(const spg_csr_t& A, const spg_csr_t& B, int& tws, int& G) {
+// `lean`: the fp64 ordered-LDS kernels (k_tile_dn / k_tile_sp) may run -- the build allows them
+// and the handle's run-time check found the LDS ordering they rely on (spg_create)
+inline bool want_tile(const spg_csr_t& A, const spg_csr_t& B, int& tws, int& G, bool lean) {
     if (A.rows == 0 || B.rows == 0 || B.cols == 0 || A.nnz == 0 || B.nnz == 0) return false;
     const double avgA = (double)A.nnz / (double)A.rows;
     const double avgB = (double)B.nnz / (double)B.rows;
@@ -225,11 +233,11 @@ inline bool want_tile(const spg_csr_t& A, const spg_csr_t& B, int& tws, int& G) 
     // fp64 C rows at least half dense and wide: dense tiles of 2048 columns (a 2048-slot
     // accumulator).  Half the items, half the segment-table lookups per product; config 4
     // measured 24.9 against 26.6 ms per product with 1024-column tiles.
-    if (B.value_type == SPG_R_64F && tws == 10 && frac >= 0.5 && B.cols >= 16384) tws = 11;
+    if (B.value_type == SPG_R_64F && lean && tws == 10 && frac >= 0.5 && B.cols >= 16384) tws = 11;
     // fp64 C rows 10-24 % dense over >= 16384 columns: sparse tiles of 8192 columns (2048-slot
     // windows; half the items, A-row reads and segment-table lookups of 4096-column tiles;
     // config 5: 149.3 -> 124.8 ms per product)
-    if (B.value_type == SPG_R_64F && SPG_TILE_LEAN && SPG_SP_LEAN && tws == 12 && frac >= 0.1 &&
+    if (B.value_type == SPG_R_64F && lean && SPG_SP_LEAN && tws == 12 && frac >= 0.1 &&
         B.cols >= 16384 && frac * 8192.0 <= 0.95 * 2048)
         tws = 13;
     // (A/B timing builds only; at most 8192 columns: k_tile_sp<.., 2048> holds 256 bitmap words)
@@ -303,6 +311,48 @@ spg_status_t hip_fail(spg_handle_t h, hipError_t e) {
     } while (0)
 
 #define SPG_LAUNCHED(h) SPG_HIP(h, hipGetLastError())
+
+// The LDS ordering the lean fp64 tile kernels rely on, checked on this device:
+// k_lds_order_check runs LDSCHK_TRIALS trials of two ds_add_f64 instructions from all 64 lanes
+// into 4 slots with operands whose rounded sums depend on the order; the host replays them in
+// (instruction, lane) order.  Any bit difference sets *ordered = false.
+hipError_t lds_order_check(bool* ordered) {
+    constexpr int N = LDSCHK_TRIALS * 2 * WAVE;
+    std::vector<double> v(N);
+    std::vector<int> slot(N);
+    uint64_t x = 0x9e3779b97f4a7c15ull;
+    auto next = [&] { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return x; };
+    for (int i = 0; i < N; ++i) {
+        const uint64_t r = next();
+        const double m = 1.0 + (double)(r >> 11) * (1.0 / 9007199254740992.0);   // [1, 2)
+        v[i] = std::ldexp((r & 1) ? -m : m, (int)((r >> 1) % 81) - 40);
+        slot[i] = (int)((r >> 8) & 3);
+    }
+    double *dv = nullptr, *dout = nullptr;
+    int* ds = nullptr;
+    hipError_t e = hipMalloc((void**)&dv, sizeof(double) * N);
+    if (e == hipSuccess) e = hipMalloc((void**)&ds, sizeof(int) * N);
+    if (e == hipSuccess) e = hipMalloc((void**)&dout, sizeof(double) * 4 * LDSCHK_TRIALS);
+    if (e == hipSuccess) e = hipMemcpy(dv, v.data(), sizeof(double) * N, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(ds, slot.data(), sizeof(int) * N, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_lds_order_check, dim3(1), dim3(WAVE), 0, 0, (const double*)dv, (const int*)ds, dout);
+        e = hipGetLastError();
+    }
+    std::vector<double> got(4 * LDSCHK_TRIALS);
+    if (e == hipSuccess) e = hipMemcpy(got.data(), dout, sizeof(double) * got.size(), hipMemcpyDeviceToHost);
+    bool ok = e == hipSuccess;
+    for (int t = 0; ok && t < LDSCHK_TRIALS; ++t) {
+        double acc[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int i = t * 2 * WAVE; i < (t + 1) * 2 * WAVE; ++i) acc[slot[i]] = acc[slot[i]] + v[i];
+        ok = std::memcmp(acc, &got[4 * t], sizeof(acc)) == 0;
+    }
+    *ordered = ok;
+    if (dv) (void)hipFree(dv);
+    if (ds) (void)hipFree(ds);
+    if (dout) (void)hipFree(dout);
+    return e;
+}
 
 hipEvent_t take_event(spg_handle_t h) {
     if (!h->pool.empty()) {
@@ -524,7 +574,7 @@ inline int64_t tile_items(const spg_plan_s& p) { return p.use_tile ? tile_rows_m
 // accumulation itself: no symbolic bitmaps, and every item's 8-byte offset is kept (all
 // rows, not one chunk's), so ALG3's numeric phase does not recompute its chunks' counts.
 inline bool tile_dense(const spg_plan_s& p) {
-    const int cap = (p.A.value_type == SPG_R_64F && SPG_TILE_LEAN) ? DN_TW_MAX : TILE_CAP;   // (k_tile_dn<.., 2048>)
+    const int cap = (p.A.value_type == SPG_R_64F && p.lean) ? DN_TW_MAX : TILE_CAP;   // (k_tile_dn<.., 2048>)
     return p.use_tile && (1 << p.tws) <= cap && tile_variant().dense;
 }
 inline int64_t tile_item_slots(const spg_plan_s& p) { return tile_dense(p) ? p.A.rows * p.G : tile_items(p); }
@@ -951,7 +1001,7 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
                                   (const int64_t*)tile_chunk_items(p, c), cj, cx, alpha);
         };
         if constexpr (OrderedLdsAdd<T>::value) {
-            if (!dense && SPG_TILE_LEAN && SPG_SP_LEAN) {   // sparse tiles, ordered LDS adds
+            if (!dense && p.lean && SPG_SP_LEAN) {   // sparse tiles, ordered LDS adds
                 auto sp = [&](auto capc) {
                     constexpr int CAP = decltype(capc)::value;
                     hipExtLaunchKernelGGL((k_tile_sp<T, IP, CAP>), dim3(tile_grid(n * p.G, SP_WPB)), dim3(SP_WPB * WAVE),
@@ -969,7 +1019,7 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
                 SPG_LAUNCHED(h);
                 continue;
             }
-            if (dense && SPG_TILE_LEAN) {   // ordered LDS adds (spgemm_tile_dn.hpp)
+            if (dense && p.lean) {   // ordered LDS adds (spgemm_tile_dn.hpp)
                 auto dn = [&](auto twd) {
                     constexpr int TWD = decltype(twd)::value;
                     // k-phased items (SPG_DN_PH, A/B builds; fp64 2048-column tiles)
@@ -1223,6 +1273,9 @@ spg_status_t spg_create(spg_handle_t* handle, int hip_device) {
     if (const char* e = std::getenv("SPG_LB_SPIN_TICKS")) h->lb_spin = std::strtoull(e, nullptr, 10);
     DeviceGuard dg_(dev);   // the handle's allocations on its device; the caller's device stays current
     hipError_t e = dg_.err;
+    if (e == hipSuccess) e = lds_order_check(&h->lds_ordered);
+    if (const char* o = std::getenv("SPG_LDS_ORDERED"))
+        if (std::strcmp(o, "0") == 0) h->lds_ordered = false;
     // fine-grained (coherent) host memory: the scan's system-scope stores of the scalars and
     // then the generation word become visible to the polling host in that order
     // (wait_mirror); the default host allocation is coarse-grained unless HIP_HOST_COHERENT=1
@@ -1287,7 +1340,8 @@ spg_status_t spg_plan(spg_handle_t h, const spg_csr_t* A, const spg_csr_t* B, sp
     tmp.seg_len = A->nnz;
     tmp.use_short = want_short(*A, *B);
     tmp.use_row = row_kernel_enabled();
-    tmp.use_tile = !tmp.use_short && want_tile(*A, *B, tmp.tws, tmp.G);
+    tmp.lean = SPG_TILE_LEAN && h->lds_ordered;
+    tmp.use_tile = !tmp.use_short && want_tile(*A, *B, tmp.tws, tmp.G, tmp.lean);
     if (tmp.use_tile) {
         tmp.TR = 1;
         tmp.twss = sym_tile_log2(*B, tmp.tws, &tmp.sym_seg);
@@ -1686,6 +1740,9 @@ spg_status_t spg_plan_info(spg_plan_t p, spg_plan_info_t* info, int64_t* chunk_r
     info->dense_tiles = tile_dense(*p) ? 1 : 0;
     const bool chunked = p->alg == SPG_ALG3 && p->chunk_rows.size() > 1;
     info->n_chunks = chunked ? (int64_t)p->chunk_rows.size() - 1 : 1;
+    // fp64 / complex128 tiles on the ordered-LDS kernels (k_tile_dn / k_tile_sp), or k_tile's
+    // owner rounds (the handle's LDS check failed, or SPG_LDS_ORDERED=0)
+    info->lds_ordered = p->use_tile && p->lean && (p->A.value_type == SPG_R_64F || p->A.value_type == SPG_C_64F) ? 1 : 0;
     for (int64_t i = 0; i < std::min<int64_t>(capacity, info->n_chunks + 1); ++i)
         chunk_rows[i] = chunked ? p->chunk_rows[(size_t)i] : (i == 0 ? 0 : p->A.rows);
     return SPG_STATUS_SUCCESS;

@@ -40,6 +40,28 @@ template <typename R> __device__ __forceinline__ void lds_add(cplx<R>* p, cplx<R
     lds_add(&p->im, v.im);
 }
 
+// Run-time check of the two properties above (spg_create, lds_order_check in spgemm.hip):
+// LDSCHK_TRIALS trials; in each, two ds_add_f64 instructions from all 64 lanes into 4 slots
+// (v and slot indexed [trial][instruction][lane]); the slots' sums go to out[trial][4].
+constexpr int LDSCHK_TRIALS = 64;
+__global__ __launch_bounds__(WAVE) void k_lds_order_check(const double* __restrict__ v, const int* __restrict__ slot,
+                                                          double* __restrict__ out) {
+    __shared__ double acc[4];
+    const int l = lane_id();
+    for (int t = 0; t < LDSCHK_TRIALS; ++t) {
+        if (l < 4) acc[l] = 0.0;
+        wsync();
+        const int i0 = t * 2 * WAVE + l, i1 = i0 + WAVE;
+        const double v0 = v[i0], v1 = v[i1];
+        const int s0 = slot[i0], s1 = slot[i1];
+        lds_add(&acc[s0], v0);
+        lds_add(&acc[s1], v1);
+        wsync();
+        if (l < 4) out[t * 4 + l] = acc[l];
+        wsync();
+    }
+}
+
 // C's stores and the streamed per-item reads (A rows, item offsets) with or without the
 // non-temporal hint (SPG_NT_C / SPG_NT_A, A/B builds), so they do not push the tile's B
 // slice out of the XCD's L2.

@@ -314,6 +314,7 @@ def plan_info(a: csr_matrix, b: csr_matrix, alg: int = 0, chunk_fraction: float 
         check(h.lib.spg_plan_info(plan, ctypes.byref(info), rows, info.n_chunks + 1), "spg_plan_info")
         return {"path": ("general", "short", "tile")[info.path], "tile_width": info.tile_width,
                 "tiles_per_row": info.tiles_per_row, "dense_tiles": bool(info.dense_tiles),
+                "lds_ordered": bool(info.lds_ordered),
                 "chunk_rows": [int(x) for x in rows]}
     finally:
         h.lib.spg_plan_destroy(plan)
