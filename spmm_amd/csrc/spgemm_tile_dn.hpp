@@ -640,6 +640,194 @@ void k_tile_sp(
     }
 }
 
+// k-phased sparse tiles (k_tile_sp's walk in PH phases of B rows, as k_tile_dn<.., PH>): the
+// block's waves (as many as the LDS holds: 7 at CAP 2048) meet at a barrier after every phase,
+// so a CU gathers from one 1/PH part of the tile's B slice at a time (config 5's 8192-column
+// slice is 25.8 MB per tile).  Items with several windows walk every window in PH phases; the
+// block runs the most windows any of its items has, idle waves joining the barriers.
+template <typename T, int CAP> constexpr int sp_ph_wpb() {
+    return (int)(158 * 1024 / (sizeof(SpLds<T, CAP>) + 16)) < 8 ? (int)(158 * 1024 / (sizeof(SpLds<T, CAP>) + 16)) : 8;
+}
+template <typename T, typename IP, int SP_CAP, int PH>
+__global__ __launch_bounds__((sp_ph_wpb<T, SP_CAP>() * WAVE)) void k_tile_sp_ph(
+    int64_t row0, int64_t nrows, int tws, int G, const IP* __restrict__ Ap,
+    const int32_t* __restrict__ Aj, const T* __restrict__ Ax, int64_t K,
+    const uint32_t* __restrict__ brec, const int32_t* __restrict__ tptr, const uint32_t* __restrict__ bitmap,
+    const int64_t* __restrict__ item_off, int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha, uint32_t sent) {
+    static_assert(OrderedLdsAdd<T>::value, "ordered LDS add needed");
+    static_assert(sizeof(T) * (SP_CAP + WAVE) >= 4 * SP_CAP, "column list fits the accumulator");
+    constexpr int SP_WPL = SpGeom<SP_CAP>::WPL;
+    constexpr int NB = sizeof(T) > 8 ? 4 : 8;
+    constexpr int WPB = sp_ph_wpb<T, SP_CAP>();
+    __shared__ __attribute__((aligned(16))) SpLds<T, SP_CAP> lds[WPB];
+    __shared__ int nwin_s[WPB];
+    const int l = lane_id();
+    const int wv = uniform((int)(threadIdx.x >> 6));
+    SpLds<T, SP_CAP>& S = lds[wv];
+    const int TW = 1 << tws;
+    const int nw = TW >> 5;
+    const int wpl = (nw + WAVE - 1) / WAVE;
+    const char* __restrict__ rb = reinterpret_cast<const char*>(brec);
+    const uint32_t items = (uint32_t)(nrows * G);
+    const bool one = alpha == (T)1;
+    for (uint32_t base = xcd_block(gridDim.x) * WPB; base < items; base += gridDim.x * WPB) {
+        const uint32_t it = base + wv;
+        bool live = it < items;
+        int g = 0, nA = 0;
+        int64_t row = 0, item = 0, a0 = 0;
+        if (live) {
+            g = (int)(it / (uint32_t)nrows);
+            row = row0 + (int64_t)(it - (uint32_t)g * (uint32_t)nrows);
+            item = (row - row0) * G + g;
+            a0 = Ap[row];
+            nA = (int)(Ap[row + 1] - a0);
+            live = nA > 0;
+        }
+        const int32_t* __restrict__ tp = tptr + (int64_t)g * (K + 1);
+        const int w0 = min(nw, l * wpl), w1 = min(nw, w0 + wpl);
+        uint32_t wd[SP_WPL] = {};
+        int mine = 0;
+        if (live) {
+            const uint32_t* __restrict__ ibits = bitmap + item * nw;
+#pragma unroll
+            for (int q = 0; q < SP_WPL; ++q)
+                if (w0 + q < w1) {
+                    wd[q] = ibits[w0 + q];
+                    mine += __popc(wd[q]);
+                }
+        }
+        const int pincl = wave_incl_sum_dpp(mine);
+        const int nnz = readlane_i(pincl, WAVE - 1);
+        live = live && nnz > 0;
+        const int p0 = pincl - mine;
+        int32_t kq[NB];
+        T aq[NB];
+        uint2 sq[NB];
+        if (!live) nA = 0;
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+            kq[q] = -1;
+            aq[q] = (T)0;
+            if (q * WAVE + l < nA) {
+                kq[q] = ld_a(Aj + a0 + q * WAVE + l);
+                aq[q] = ld_a(Ax + a0 + q * WAVE + l);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < NB; ++q) sq[q] = kq[q] >= 0 ? seg_pair(tp, kq[q]) : make_uint2(0u, 0u);
+        const int64_t obase = live ? item_off[item] : 0;
+        wsync();
+        if (live) {
+            int run = p0;
+#pragma unroll
+            for (int q = 0; q < SP_WPL; ++q)
+                if (w0 + q < w1) {
+                    S.bw[w0 + q] = make_uint2(wd[q], (uint32_t)run);
+                    run += __popc(wd[q]);
+                }
+        }
+        // the item's windows: lanes [L0, L1) whose words' entries fit SP_CAP slots
+        auto window_end = [&](int L0) {
+            if (nnz <= SP_CAP) return WAVE;
+            const int wb = readlane_i(p0, L0);
+            int L1 = (int)__popcll(__ballot(pincl <= wb + SP_CAP));
+            return L1 <= L0 ? L0 + 1 : L1;
+        };
+        int nwin = 0;
+        if (live)
+            for (int L0 = 0; L0 < WAVE; L0 = window_end(L0)) ++nwin;
+        if (l == 0) nwin_s[wv] = nwin;
+        __syncthreads();
+        int maxwin = 0;
+#pragma unroll
+        for (int q = 0; q < WPB; ++q) maxwin = max(maxwin, nwin_s[q]);
+        const int lo = g * TW;
+        int L0 = 0;
+        for (int w = 0; w < maxwin; ++w) {
+            const bool act = w < nwin;   // (nwin = 0 for dead waves)
+            int L1 = WAVE, wb = 0, wn = nnz;
+            if (act) {
+                L1 = window_end(L0);
+                if (nnz > SP_CAP) {
+                    wb = readlane_i(p0, L0);
+                    wn = (L1 < WAVE ? readlane_i(p0, L1) : nnz) - wb;
+                }
+                wsync();
+                for (int p = l; p < wn; p += WAVE) S.acc[p] = (T)0;
+            }
+            const int clo = 32 * wpl * L0, chi = 32 * wpl * L1;   // window, tile-relative
+            for (int ph = 0; ph < PH; ++ph) {
+                if (act) {
+                    const int klo = (int)(K * ph / PH), khi = (int)(K * (ph + 1) / PH);
+                    int32_t kc[NB];
+                    T ac[NB];
+                    uint2 sc[NB];
+#pragma unroll
+                    for (int q = 0; q < NB; ++q) {
+                        kc[q] = kq[q];
+                        ac[q] = aq[q];
+                        sc[q] = sq[q];
+                    }
+                    dn_walk<T, NB, true>(&S, S.acc, l, tp, a0, nA, ac, sc, Aj, Ax, rb, sent,
+                                         [&](int rc) -> int {
+                                             if (rc < clo || rc >= chi) return SP_CAP + l;   // (sentinels too)
+                                             const uint2 b = S.bw[rc >> 5];
+                                             return (int)b.y + __popc(b.x & ((1u << (rc & 31)) - 1u)) - wb;
+                                         },
+                                         [&](int) {}, &kc, klo, khi);
+                }
+                __syncthreads();
+            }
+            if (act && (SPG_TILE_DIAG & 8) == 0) {
+                wsync();
+                T* __restrict__ xw = Cx + obase + wb;
+                auto vals = [&](auto one) {
+                    for (int q0 = 0; q0 < wn; q0 += 4 * WAVE) {
+                        T v[4];
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) v[e] = S.acc[min(q0 + e * WAVE + l, SP_CAP + WAVE - 1)];
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const int p = q0 + e * WAVE + l;
+                            if (p < wn) st_c(xw + p, decltype(one)::value ? v[e] : mul_rn(alpha, v[e]));
+                        }
+                    }
+                };
+                if (one) vals(std::true_type{});
+                else vals(std::false_type{});
+                wsync();
+                uint32_t* __restrict__ cl = reinterpret_cast<uint32_t*>(S.acc);
+                if (l >= L0 && l < L1) {
+                    int pos = p0 - wb;
+#pragma unroll
+                    for (int q = 0; q < SP_WPL; ++q) {
+                        uint32_t x = wd[q];
+                        const int cb = lo + 32 * (w0 + q);
+                        while (x != 0u) {
+                            cl[pos++] = (uint32_t)(cb + __builtin_ctz(x));
+                            x &= x - 1u;
+                        }
+                    }
+                }
+                wsync();
+                int32_t* __restrict__ cw = Cj + obase + wb;
+                for (int q0 = 0; q0 < wn; q0 += 4 * WAVE) {
+                    uint32_t v[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = cl[min(q0 + e * WAVE + l, SP_CAP - 1)];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int p = q0 + e * WAVE + l;
+                        if (p < wn) st_c(cw + p, (int32_t)v[e]);
+                    }
+                }
+            }
+            L0 = L1;
+        }
+        __syncthreads();   // (nwin_s is rewritten next round)
+    }
+}
+
 // ---------------------------------------------------------------------------------------
 // Symbolic pass over long B segments (a symbolic tile's expected segment >= SEG_MIN = 128 entries:
 // config 4's whole rows of 328 columns).  The bitmap OR is order-free, so there is no lane ->

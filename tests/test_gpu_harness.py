@@ -115,3 +115,27 @@ def test_dpeak_sampler_sees_the_product():
     peak, lib = json.loads(r.stdout.strip().splitlines()[-1])
     assert lib and lib > 4e8
     assert peak >= 0.9 * lib, (peak, lib)
+
+
+@pytest.mark.parametrize("chunks_forced", [False, True])
+def test_numerical_error_ports_alg1_equals_alg3(chunks_forced):
+    """numerical_error/error.py and fraction.py (the reference's ALG1-vs-ALG3 error checks,
+    error.py:16-30 at chunk_fraction 0.3, fraction.py's chunk_fraction sweep) through the ports:
+    every max |ALG1 - ALG3| is exactly 0, with ALG3's chunks as planned and with them forced
+    (SPG_ALG3_CHUNK_ALWAYS=1).  fraction.py runs at density 0.1 -- the reference's
+    `density = 0.` (fraction.py:8) would multiply empty matrices."""
+    env = {"SPG_ALG3_CHUNK_ALWAYS": "1"} if chunks_forced else {}
+    d = os.path.join(H, "numerical_error")
+    r = subprocess.run([sys.executable, "error.py"], capture_output=True, text=True, timeout=600, cwd=d,
+                       env=dict(os.environ, **env))
+    assert r.returncode == 0, r.stderr[-2000:]
+    rows = [ln.split() for ln in r.stdout.splitlines() if ln.strip() and ln.split()[0].isdigit()]
+    assert len(rows) == 9, r.stdout
+    assert all(float(x[2]) == 0.0 for x in rows), r.stdout          # |alg1 - alg3|
+    assert all(float(x[3]) < 1e-2 for x in rows), r.stdout          # fp32 against an fp64 reference
+    r = subprocess.run([sys.executable, "fraction.py"], capture_output=True, text=True, timeout=600, cwd=d,
+                       env=dict(os.environ, **env))
+    assert r.returncode == 0, r.stderr[-2000:]
+    rows = [ln.split() for ln in r.stdout.splitlines() if ln.strip() and ln.split()[0][0].isdigit()]
+    assert len(rows) == 8, r.stdout
+    assert all(float(x[1]) == 0.0 for x in rows), r.stdout
