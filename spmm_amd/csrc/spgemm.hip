@@ -623,7 +623,7 @@ Layout make_layout(const spg_plan_s& p) {
         L.items = off; off = align_up(off + sizeof(int64_t) * (size_t)(tile_item_slots(p) + 1));
         // B's column indices modulo 65536 (the symbolic pass's columns: a symbolic tile never
         // crosses a 65536-aligned block)
-        L.bj16 = off;  off = align_up(off + sizeof(uint16_t) * (size_t)(p.B.nnz + 2));   // (+2: whole words)
+        L.bj16 = off;  off = align_up(off + sizeof(uint16_t) * (size_t)(p.B.nnz + 8));   // (+8: whole 16-byte loads)
         // item bitmaps; before the first symbolic pass the region holds the row-major
         // boundary index the tile-major B is built from
         const size_t bm = tile_dense(p) ? 0 : sizeof(uint32_t) * (size_t)tile_items(p) * (size_t)((1 << p.tws) >> 5);

@@ -128,10 +128,19 @@ template <typename T, int TWD, bool HIT = !dn_sent<T>()> struct DnLds {
 };
 // (dn_sent, TWD 1024: 10,000 bytes per wave -- 8 two-wave blocks, 16 waves, fit a CU's 160 KB;
 // TWD 2048: 18,192 bytes, 8 waves)
+// SPG_DN_WIDE: the output leaves in 16-byte stores (dn_emit_wide): the item's entries are first
+// compacted in LDS (values in place in acc, u16 columns in cols), a quarter of the store
+// instructions of one 4-byte and one 8-byte store per entry.
+#ifndef SPG_DN_WIDE
+#define SPG_DN_WIDE 0
+#endif
 template <typename T, int TWD> struct DnLds<T, TWD, false> {
     T acc[TWD + DN_DUMMY];
     DnEnt<T> ent[WAVE + 1];
     uint8_t mk[NUM_MK];
+#if SPG_DN_WIDE
+    uint16_t cols[TWD + 8];       // compacted columns (tile-relative), shifted to align the stores
+#endif
 #ifdef SPG_LDS_PAD
     uint8_t pad[SPG_LDS_PAD];   // (A/B builds: occupancy sensitivity)
 #endif
@@ -342,6 +351,79 @@ __device__ __forceinline__ void dn_emit(DnLds<T, TWD>& S, int l, int TW, int lo,
     }
 }
 
+#if SPG_DN_WIDE
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void st_c4(int32_t* p, i32x4 v) {
+    if constexpr (SPG_NT_C != 0) __builtin_nontemporal_store(v, reinterpret_cast<i32x4*>(p));
+    else *reinterpret_cast<i32x4*>(p) = v;
+}
+__device__ __forceinline__ void st_c2(double* p, f64x2 v) {
+    if constexpr (SPG_NT_C != 0) __builtin_nontemporal_store(v, reinterpret_cast<f64x2*>(p));
+    else *reinterpret_cast<f64x2*>(p) = v;
+}
+
+// The item's output with 16-byte stores (fp64 dense tiles, dn_sent): the slots that left -0.0
+// are compacted in column order -- the values in place in acc (an entry's position never
+// exceeds its column, and every 4-group round reads its slots before it writes), the columns
+// as u16 in cols shifted so that the 4-aligned output quads start 8-byte aligned -- then the
+// columns leave as int32 quads and the values as pairs, the unaligned head and tail entry by
+// entry.  Returns the entries found; fewer than nnz (a column reached only by -0.0 products)
+// writes nothing: the caller redoes the item through dn_item's re-walk.
+template <int TWD>
+__device__ __forceinline__ int dn_emit_wide(DnLds<double, TWD>& S, int l, int TW, int lo, int nnz, int64_t obase,
+                                            int32_t* __restrict__ Cj, double* __restrict__ Cx, double alpha) {
+    const int ch = (int)((4 - (obase & 3)) & 3);    // column entries before the first 16-byte boundary
+    const int co = 4 - ch;                          // cols[p + co]: quads at 8-byte aligned LDS offsets
+    const bool one = alpha == 1.0;
+    wsync();
+    int run = 0;
+    for (int k0 = 0; k0 < TW / WAVE; k0 += 4) {
+        double v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = S.acc[(k0 + e) * WAVE + l];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const bool h = !is_neg_zero(v[e]);
+            const unsigned long long m = __ballot(h);
+            if (h) {
+                const int p = run + lane_rank(m);
+                S.acc[p] = one ? v[e] : mul_rn(alpha, v[e]);
+                S.cols[p + co] = (uint16_t)((k0 + e) * WAVE + l);
+            }
+            run += (int)__popcll(m);
+        }
+    }
+    if (run < nnz || (SPG_TILE_DIAG & 8) != 0) return run;
+    wsync();
+    int32_t* __restrict__ crow = Cj + obase;
+    double* __restrict__ xrow = Cx + obase;
+    // columns: head entries [0, ch), quads [ch + 4i, ch + 4i + 4), tail
+    const int nq = (run - ch) >> 2;
+    if (l < ch && l < run) st_c(crow + l, (int32_t)(lo + S.cols[l + co]));
+    for (int i = l; i < nq; i += WAVE) {
+        const uint2 w = *reinterpret_cast<const uint2*>(&S.cols[4 * i + 4]);
+        const i32x4 c4 = {lo + (int)(w.x & 0xffffu), lo + (int)(w.x >> 16), lo + (int)(w.y & 0xffffu), lo + (int)(w.y >> 16)};
+        st_c4(crow + ch + 4 * i, c4);
+    }
+    {
+        const int t = ch + 4 * nq + l;
+        if (nq >= 0 && l < 4 && t < run && t >= ch) st_c(crow + t, (int32_t)(lo + S.cols[t + co]));
+    }
+    // values: head entry [0, vh), pairs [vh + 2i, vh + 2i + 2), tail
+    const int vh = (int)(obase & 1);
+    const int np = (run - vh) >> 1;
+    if (l < vh && l < run) st_c(xrow + l, S.acc[l]);
+    for (int i = l; i < np; i += WAVE) {
+        const int q = vh + 2 * i;
+        const f64x2 x2 = {S.acc[q], S.acc[q + 1]};
+        st_c2(xrow + q, x2);
+    }
+    if (l == 0 && np >= 0 && vh + 2 * np < run) st_c(xrow + vh + 2 * np, S.acc[vh + 2 * np]);
+    return run;
+}
+#endif
+
 // clear an item's accumulator
 template <typename T, int TWD>
 __device__ __forceinline__ void dn_clear(DnLds<T, TWD>& S, int l, int TW) {
@@ -438,7 +520,42 @@ __global__ __launch_bounds__(dn_wpb<PH>() * WAVE) void k_tile_dn(
         }
 #pragma unroll
         for (int q = 0; q < NB; ++q) sq[q] = kq[q] >= 0 ? seg_pair(tp, kq[q]) : make_uint2(0u, 0u);
+        if constexpr ((SPG_TILE_DIAG & 64) != 0) {   // timing only: no segment-table lookups
+            const uint32_t s0 = (uint32_t)tp[0], s1 = (uint32_t)tp[K];
+#pragma unroll
+            for (int q = 0; q < NB; ++q) {
+                const uint32_t st = s0 + ((uint32_t)kq[q] * 2654435761u) % max(1u, s1 - s0 - 11u);
+                sq[q] = kq[q] >= 0 ? make_uint2(st, st + 10u) : make_uint2(0u, 0u);
+            }
+        }
         if constexpr (PH == 1) {
+#if SPG_DN_WIDE
+            if constexpr (std::is_same<T, double>::value) {
+                dn_clear(S, l, TW);
+                int32_t kc[NB];
+                dn_walk<T, NB>(&S, S.acc, l, tp, a0, nA, aq, sq, Aj, Ax, rb, sent, [&](int c) { return c; },
+                               [&](int) {});
+                if (dn_emit_wide<TWD>(S, l, TW, g * TW, nnz, obase, Cj, Cx, alpha) < nnz &&
+                    (SPG_TILE_DIAG & 9) == 0) {
+                    // rare: a column reached only by -0.0 products -- the item again through
+                    // dn_item (its re-walk turns such slots into scipy's +0.0)
+#pragma unroll
+                    for (int q = 0; q < NB; ++q) {
+                        kc[q] = -1;
+                        aq[q] = (T)0;
+                        if (q * WAVE + l < nA) {
+                            kc[q] = Aj[a0 + q * WAVE + l];
+                            aq[q] = Ax[a0 + q * WAVE + l];
+                        }
+                    }
+#pragma unroll
+                    for (int q = 0; q < NB; ++q) sq[q] = kc[q] >= 0 ? seg_pair(tp, kc[q]) : make_uint2(0u, 0u);
+                    dn_item<T, NB, TWD>(S, l, TW, g * TW, nnz, tp, a0, nA, aq, sq, Aj, Ax, rb, sent, Cj + obase,
+                                        Cx + obase, alpha);
+                }
+                continue;
+            }
+#endif
             dn_item<T, NB, TWD>(S, l, TW, g * TW, nnz, tp, a0, nA, aq, sq, Aj, Ax, rb, sent, Cj + obase, Cx + obase,
                                 alpha);
         } else {
@@ -829,11 +946,13 @@ __global__ __launch_bounds__((sp_ph_wpb<T, SP_CAP>() * WAVE)) void k_tile_sp_ph(
 }
 
 // ---------------------------------------------------------------------------------------
-// Symbolic pass over long B segments (a symbolic tile's expected segment >= SEG_MIN = 128 entries:
-// config 4's whole rows of 328 columns).  The bitmap OR is order-free, so there is no lane ->
-// product map: four A entries per instruction, one per 16-lane group, each group walking its
-// entry's B segment 32 columns (one 4-byte word of two 2-byte columns per lane, k_bj16) at a
-// time, 8 steps in flight.
+// Symbolic pass over long B segments (a symbolic tile's expected segment >= SEG_MIN entries:
+// config 4's whole rows of 328 columns, config 5's 65-column quarters).  The bitmap OR is
+// order-free, so there is no lane -> product map: four A entries per instruction, one per
+// 16-lane group, each group walking its entry's B segment 128 columns (one 16-byte load of
+// eight 2-byte columns per lane, k_bj16) at a time, four entries per group in flight.  (Round 4: 16-byte
+// loads -- a wave load costs the same per instruction whether it moves 4 or 16 bytes per lane,
+// abtest/gather_probe -- instead of 4-byte ones: a quarter of the load instructions.)
 // Writes each numeric tile's entry count (and, for sparse numeric tiles, its bitmap), as
 // k_tile_sym.  (Measured on config 4: 4.05 ms against 7.05 ms for k_tile_sym's flattened
 // walk over 16384-column tiles and 7.0 ms for a one-entry-per-instruction cursor walk.)
@@ -843,7 +962,7 @@ __global__ __launch_bounds__(SEG_WPB * WAVE) void k_tile_sym_seg(
     int64_t row0, int64_t nrows, int tws, int G, int twss, const IP* __restrict__ Ap,
     const int32_t* __restrict__ Aj, const IP* __restrict__ Bp, const uint16_t* __restrict__ Bj16,
     const uint32_t* __restrict__ sidx, uint32_t* __restrict__ bitmap, int64_t* __restrict__ item_cnt) {
-    constexpr int U = 8;
+    constexpr int NQ = 4;   // quads of A entries per round: 16 entries, 4 loads in flight per lane
     __shared__ __attribute__((aligned(16))) uint32_t bits_all[SEG_WPB][SYM_NWMAX];
     const int l = lane_id();
     const int sub = l & 15, grp = l >> 4;
@@ -869,47 +988,72 @@ __global__ __launch_bounds__(SEG_WPB * WAVE) void k_tile_sym_seg(
         wsync();
         for (int w = l; w < nws; w += WAVE) bits[w] = 0u;
         wsync();
-        for (int b = 0; b < nA; b += 4) {   // entries b .. b+3, one per 16-lane group
-            int cnt = 0;
-            int64_t beg = 0;
-            if (b + grp < nA) {
-                const int32_t k = Aj[a0 + b + grp];
-                const IP rb = Bp[k];
-                if (Gs == 1) {
-                    cnt = (int)(Bp[k + 1] - rb);
-                    beg = (int64_t)rb;
-                } else {
-                    const uint32_t* sk = sidx + (int64_t)k * (Gs + 1);
-                    const uint32_t s0 = sk[gs];
-                    cnt = (int)(sk[gs + 1] - s0);
-                    beg = (int64_t)rb + s0;
+        // NQ quads of entries (4 per quad, one per 16-lane group) per round; the next round's
+        // segment extents (A column -> B row start -> symbolic-tile start) are loaded while
+        // this round's columns are in flight
+        auto extents = [&](int b, int (&cnt)[NQ], int64_t (&beg)[NQ]) {
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                cnt[q] = 0;
+                beg[q] = 0;
+                const int e = b + 4 * q + grp;
+                if (e < nA) {
+                    const int32_t k = Aj[a0 + e];
+                    const IP rb = Bp[k];
+                    if (Gs == 1) {
+                        cnt[q] = (int)(Bp[k + 1] - rb);
+                        beg[q] = (int64_t)rb;
+                    } else {
+                        const uint32_t* sk = sidx + (int64_t)k * (Gs + 1);
+                        const uint32_t s0 = sk[gs];
+                        cnt[q] = (int)(sk[gs + 1] - s0);
+                        beg[q] = (int64_t)rb + s0;
+                    }
                 }
             }
-            // two 16-bit columns per lane per load: the segment from its even-aligned start b0
-            // (span = cnt + (beg & 1) elements; a word's element before beg or past the
-            // segment is skipped; the region is padded, so the last word stays inside it).
-            // The longest of the four spans sets the steps (wave-uniform).
-            const int odd = (int)(beg & 1);
-            const int span = cnt + odd;
-            const uint32_t* __restrict__ w0 = reinterpret_cast<const uint32_t*>(Bj16 + (beg - odd));
-            int mx = span;
+        };
+        int cnt[NQ];
+        int64_t beg[NQ];
+        extents(0, cnt, beg);
+        for (int b = 0; b < nA; b += 4 * NQ) {
+            // eight 16-bit columns per lane per 16-byte load: each segment from its 8-aligned
+            // start (span = cnt + (beg & 7) elements; an element before beg or past the segment
+            // is skipped; the region is padded, so the last load stays inside it).  A 16-lane
+            // group covers 128 columns per step; the longest span of the round sets the steps.
+            int odd[NQ], span[NQ];
+            const uint4* __restrict__ w0[NQ];
+            int mx = 0;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                odd[q] = (int)(beg[q] & 7);
+                span[q] = cnt[q] + odd[q];
+                w0[q] = reinterpret_cast<const uint4*>(Bj16 + (beg[q] - odd[q]));
+                mx = max(mx, span[q]);
+            }
             mx = max(mx, __shfl_xor(mx, 16, WAVE));
             mx = max(mx, __shfl_xor(mx, 32, WAVE));
             mx = uniform(mx);
-            for (int e = 0; e < mx; e += 32 * U) {
-                uint32_t w[U];
+            for (int e = 0; e < mx; e += 128) {
+                uint4 w[NQ];
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int x = e + 32 * u + 2 * sub;
-                    w[u] = x < span ? w0[x >> 1] : 0u;
+                for (int q = 0; q < NQ; ++q) {
+                    const int x = e + 8 * sub;
+                    w[q] = x < span[q] ? w0[q][x >> 3] : make_uint4(0u, 0u, 0u, 0u);
                 }
+                if (e == 0) extents(b + 4 * NQ, cnt, beg);   // (next round; span/odd/w0 are kept)
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int x = e + 32 * u + 2 * sub;
-                    if (x >= odd && x < span) set_bit(bits, (int)(w[u] & 0xffffu) - lo16);
-                    if (x + 1 < span) set_bit(bits, (int)(w[u] >> 16) - lo16);
+                for (int q = 0; q < NQ; ++q) {
+                    const int x = e + 8 * sub;
+                    const uint32_t ww[4] = {w[q].x, w[q].y, w[q].z, w[q].w};
+#pragma unroll
+                    for (int h = 0; h < 8; ++h) {
+                        const int xh = x + h;
+                        if (xh >= odd[q] && xh < span[q])
+                            set_bit(bits, (int)((ww[h >> 1] >> (16 * (h & 1))) & 0xffffu) - lo16);
+                    }
                 }
             }
+            if (mx == 0) extents(b + 4 * NQ, cnt, beg);
         }
         wsync();
         if (bitmap) {
