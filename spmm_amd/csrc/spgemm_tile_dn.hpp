@@ -351,7 +351,10 @@ __device__ __forceinline__ void dn_emit(DnLds<T, TWD>& S, int l, int TW, int lo,
     }
 }
 
-#if SPG_DN_WIDE
+#ifndef SPG_SP_WIDE
+#define SPG_SP_WIDE 0
+#endif
+#if SPG_DN_WIDE || SPG_SP_WIDE
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void st_c4(int32_t* p, i32x4 v) {
@@ -362,6 +365,8 @@ __device__ __forceinline__ void st_c2(double* p, f64x2 v) {
     if constexpr (SPG_NT_C != 0) __builtin_nontemporal_store(v, reinterpret_cast<f64x2*>(p));
     else *reinterpret_cast<f64x2*>(p) = v;
 }
+#endif
+#if SPG_DN_WIDE
 
 // The item's output with 16-byte stores (fp64 dense tiles, dn_sent): the slots that left -0.0
 // are compacted in column order -- the values in place in acc (an entry's position never
@@ -647,12 +652,22 @@ void k_tile_sp(
         const int w0 = min(nw, l * wpl), w1 = min(nw, w0 + wpl);
         uint32_t wd[SP_WPL] = {};
         int mine = 0;
+        if (SP_WPL == 4 && wpl == 4) {   // (8192-column tiles: a lane's 4 words in one 16-byte load)
+            const uint4 w4 = *reinterpret_cast<const uint4*>(ibits + w0);
+            wd[0] = w4.x;
+            wd[1 % SP_WPL] = w4.y;
+            wd[2 % SP_WPL] = w4.z;
+            wd[3 % SP_WPL] = w4.w;
 #pragma unroll
-        for (int q = 0; q < SP_WPL; ++q)
-            if (w0 + q < w1) {
-                wd[q] = ibits[w0 + q];
-                mine += __popc(wd[q]);
-            }
+            for (int q = 0; q < SP_WPL; ++q) mine += __popc(wd[q]);
+        } else {
+#pragma unroll
+            for (int q = 0; q < SP_WPL; ++q)
+                if (w0 + q < w1) {
+                    wd[q] = ibits[w0 + q];
+                    mine += __popc(wd[q]);
+                }
+        }
         const int pincl = wave_incl_sum_dpp(mine);
         const int nnz = readlane_i(pincl, WAVE - 1);
         if (nnz == 0) continue;
@@ -707,7 +722,60 @@ void k_tile_sp(
                            },
                            [&](int) {});
             wsync();
-            if ((SPG_TILE_DIAG & 8) == 0) {   // (diag 8, timing only: no output)
+#if SPG_SP_WIDE
+            constexpr bool wide = std::is_same<T, double>::value;
+#else
+            constexpr bool wide = false;
+#endif
+            if constexpr (wide) {
+              if ((SPG_TILE_DIAG & 8) == 0) {
+                // 16-byte stores: the values straight from the compact accumulator as pairs, the
+                // columns listed into the freed accumulator (shifted so that 4-aligned output
+                // quads sit at 16-byte LDS offsets) and stored as int32 quads; unaligned heads
+                // and tails entry by entry
+                const int64_t ob = obase + wb;
+                double* __restrict__ xw = reinterpret_cast<double*>(Cx) + ob;
+                const double* acc = reinterpret_cast<const double*>(S.acc);
+                const int vh = (int)(ob & 1);
+                const int np = (wn - vh) >> 1;
+                const double al = (double)alpha;
+                if (l < vh && l < wn) st_c(xw + l, one ? acc[l] : mul_rn(al, acc[l]));
+                for (int i = l; i < np; i += WAVE) {
+                    const int q = vh + 2 * i;
+                    f64x2 x2 = {acc[q], acc[q + 1]};
+                    if (!one) x2 = f64x2{mul_rn(al, x2.x), mul_rn(al, x2.y)};
+                    st_c2(xw + q, x2);
+                }
+                if (l == 0 && np >= 0 && vh + 2 * np < wn) st_c(xw + vh + 2 * np, one ? acc[vh + 2 * np] : mul_rn(al, acc[vh + 2 * np]));
+                wsync();
+                const int ch = (int)((4 - (ob & 3)) & 3), co = 4 - ch;
+                uint32_t* __restrict__ cl = reinterpret_cast<uint32_t*>(S.acc);
+                if (l >= L0 && l < L1) {
+                    int pos = p0 - wb + co;
+#pragma unroll
+                    for (int q = 0; q < SP_WPL; ++q) {
+                        uint32_t w = wd[q];
+                        const int cb = lo + 32 * (w0 + q);
+                        while (w != 0u) {
+                            cl[pos++] = (uint32_t)(cb + __builtin_ctz(w));
+                            w &= w - 1u;
+                        }
+                    }
+                }
+                wsync();
+                int32_t* __restrict__ cw = Cj + ob;
+                const int nq = (wn - ch) >> 2;
+                if (l < ch && l < wn) st_c(cw + l, (int32_t)cl[l + co]);
+                for (int i = l; i < nq; i += WAVE) {
+                    const uint4 c4 = *reinterpret_cast<const uint4*>(&cl[4 * i + 4]);
+                    st_c4(cw + ch + 4 * i, i32x4{(int)c4.x, (int)c4.y, (int)c4.z, (int)c4.w});
+                }
+                {
+                    const int t = ch + 4 * nq + l;
+                    if (nq >= 0 && l < 4 && t < wn && t >= ch) st_c(cw + t, (int32_t)cl[t + co]);
+                }
+              }
+            } else if ((SPG_TILE_DIAG & 8) == 0) {   // (diag 8, timing only: no output)
                 // values: the window's slots are its entries in C order
                 T* __restrict__ xw = Cx + obase + wb;
                 auto vals = [&](auto one) {   // 4 rows of 64 slots per round, reads first

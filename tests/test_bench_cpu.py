@@ -35,12 +35,16 @@ def test_committed_traffic_is_stamped():
         assert db[key]["hbm_bytes_per_launch"] > 0
 
 
-def test_bench_spawns_ranks_without_launcher(tmp_path):
-    """`python3 bench.py --gpus 2` with no WORLD_SIZE (the driver's SCALE command): the parent
-    starts two worker ranks itself (gloo here, --device cpu, the oracle as the per-rank
+import pytest
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_spawns_ranks_without_launcher(tmp_path, world):
+    """`python3 bench.py --gpus N` with no WORLD_SIZE (the driver's SCALE command), N = 2 and 4:
+    the parent starts N worker ranks itself (gloo here, --device cpu, the oracle as the per-rank
     multiply hook) and rank 0 prints ONE JSON line.  Both workloads are checked against the
-    oracle on the global matrices: config 4 weak-scaled (rank r owns rows [r*n, (r+1)*n) of a
-    2n x n A) and config 5 strong-scaled (one n5 x n5 A cut on the product prefix, each rank
+    oracle on the global matrices: config 4 weak-scaled (rank r owns rows [r*n, (r+1)*n) of an
+    N*n x n A) and config 5 strong-scaled (one n5 x n5 A cut on the product prefix, each rank
     drawing only its block)."""
     import os
     import subprocess
@@ -57,7 +61,7 @@ def test_bench_spawns_ranks_without_launcher(tmp_path):
     env = dict(os.environ, SPG_BENCH_HOOK_DUMP=dump, PYTHONPATH=bench.ROOT)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
-    cmd = [sys.executable, os.path.join(bench.ROOT, "bench.py"), "--gpus", "2", "--device", "cpu",
+    cmd = [sys.executable, os.path.join(bench.ROOT, "bench.py"), "--gpus", str(world), "--device", "cpu",
            "--multiply-hook", "tests.bench_hooks:oracle_multiply", "--n", str(n), "--config5-n", str(n5),
            "--steps", "2", "--warmup", "1", "--cpu-seconds", "0"]
     r = subprocess.run(cmd, env=env, cwd=bench.ROOT, capture_output=True, text=True, timeout=300)
@@ -65,12 +69,12 @@ def test_bench_spawns_ranks_without_launcher(tmp_path):
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout
     line = json.loads(lines[0])
-    assert line["n_gpus"] == 2 and line["steps"] == 2 and line["warmup"] == 1
+    assert line["n_gpus"] == world and line["steps"] == 2 and line["warmup"] == 1
     assert line["scaling"] == "weak" and line["config"]["rows_per_rank"] == n
     assert line["config5"]["scaling"] == "strong"
 
     def stitched(nn):
-        parts = [np.load(f"{dump}.n{nn}.rank{k}.npz") for k in range(2)]
+        parts = [np.load(f"{dump}.n{nn}.rank{k}.npz") for k in range(world)]
         base, ps = 0, [np.zeros(1, np.int64)]
         for q in parts:
             ps.append(q["p"][1:].astype(np.int64) + base)
@@ -79,8 +83,8 @@ def test_bench_spawns_ranks_without_launcher(tmp_path):
                 np.concatenate([q["x"] for q in parts]))
 
     cpu = torch.device("cpu")
-    # config 4, weak: the global A is 2n x n
-    A = gen.random_csr(2 * n, n, 5e-3, seed=42, device=cpu).get()
+    # config 4, weak: the global A is (world * n) x n
+    A = gen.random_csr(world * n, n, 5e-3, seed=42, device=cpu).get()
     B = gen.random_csr(n, n, 5e-3, seed=43, device=cpu).get()
     rp, rj, rx = oracle.spgemm(A, B, keep_zeros=True, sort=True)
     p, j, x = stitched(n)
