@@ -1,4 +1,3 @@
-VARIANTS="ph1 wide d8 d2 d1 d64 ph1 wide" bash abtest/ab_c4.sh > gpurun_out/ab_diag.log 2>&1; echo rc=$?; cat gpurun_out/ab_diag.log
-VARIANTS="ph1 spw ph1 spw" bash abtest/ab_c5.sh > gpurun_out/ab_spw.log 2>&1; echo rc=$?; cat gpurun_out/ab_spw.log
-SPG_LIB=$PWD/spmm_amd/lib/libv_wide.so timeout -k 10 600 python -u -m pytest tests/test_gpu_configs.py tests/test_gpu_parity.py -k "65536 or config3 or dense_2048 or negative_zero or golden or random" -x -q --timeout 250 --timeout-method thread > gpurun_out/wide_tests.log 2>&1; echo t_rc=$?; tail -n 3 gpurun_out/wide_tests.log
-SPG_LIB=$PWD/spmm_amd/lib/libv_spw.so timeout -k 10 600 python -u -m pytest tests/test_gpu_configs.py tests/test_gpu_parity.py -k "262144-0.001-2 or sparse_8192 or golden or random or windows" -x -q --timeout 250 --timeout-method thread > gpurun_out/spw_tests.log 2>&1; echo t_rc=$?; tail -n 3 gpurun_out/spw_tests.log
+VARIANTS="rec10 r10ntr ph1 rec10" bash abtest/ab_c5.sh > gpurun_out/ab_ntr.log 2>&1; echo rc=$?; cat gpurun_out/ab_ntr.log
+VARIANTS="ph1 rec10 r10ntr" bash abtest/pmc_c5.sh > gpurun_out/pmc5.log 2>&1; echo rc=$?; cat gpurun_out/pmc5.log
+VARIANTS="rec10nta r10ntr" CFG=4 bash abtest/pmc_c5.sh > gpurun_out/pmc4.log 2>&1; echo rc=$?; cat gpurun_out/pmc4.log

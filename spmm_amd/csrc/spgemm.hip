@@ -133,7 +133,7 @@ inline size_t vbytes(spg_dtype_t t) {
 }
 
 // bytes of one tile-major B record of the tile path (column in tile + value, unpadded)
-inline size_t brec_bytes(spg_dtype_t t) { return 4 + vbytes(t); }
+inline size_t brec_bytes(spg_dtype_t t) { return (SPG_REC10 && t == SPG_R_64F) ? 10 : 4 + vbytes(t); }
 
 // Runs f(T{}) with T the C++ type of value type t.
 // (SPG_ONLY_F64: fp64-only development builds for A/B timing, about 3x faster to compile;
@@ -982,7 +982,7 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
     }
     // byte offset of sentinel region r after B's records (k_bt_pack)
     auto sent = [&](int r) {
-        return (uint32_t)(((uint64_t)p.B.nnz + (uint64_t)r * SENT_N) * sizeof(uint32_t) * rec_words<T>());
+        return (uint32_t)(((uint64_t)p.B.nnz + (uint64_t)r * SENT_N) * (uint64_t)rec_bytes<T>());
     };
     const int64_t nch = tile_chunks(p);
     for (int64_t c = 0; c < nch; ++c) {

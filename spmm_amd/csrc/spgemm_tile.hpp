@@ -107,10 +107,43 @@ __global__ __launch_bounds__(256) void k_tile_index(int64_t rows, const IP* __re
 // Offsets are 32-bit byte offsets from the (scalar) base: the host keeps the record array
 // under 4 GiB on the tile path.
 template <typename T> constexpr int rec_words() { return 1 + (int)(sizeof(T) / 4); }
+// SPG_REC10 (round 4, default): fp64 records of 10 bytes -- the value, then the column inside the
+// tile as u16 (tiles
+// are at most 8192 columns wide, sentinel columns below 65536) -- packed without padding, so a
+// tile's slice is 5/6 of the 12-byte form (config 4's 2048-column slice 8.0 -> 6.7 MB against an
+// XCD's 4 MB L2).  Record i starts at byte 10i, which is 0 or 2 modulo 4: one dwordx3 load from
+// the dword below it holds the whole record, and two v_alignbit and a shift take it apart.
+// Measured (A/B on one box): config 4 numeric 20.7 -> 19.8 ms, config 5 103.7 -> 98.7 ms.
+#ifndef SPG_REC10
+#define SPG_REC10 1
+#endif
+// SPG_NT_REC (A/B builds): the 10-byte record gathers as non-temporal loads
+#ifndef SPG_NT_REC
+#define SPG_NT_REC 0
+#endif
+template <typename T> constexpr int rec_bytes() {
+    return (SPG_REC10 && std::is_same<T, double>::value) ? 10 : 4 * rec_words<T>();
+}
 
 template <typename T, typename IP>
 __device__ __forceinline__ void load_rec(const uint32_t* __restrict__ rec, IP i, int& lc, T& v) {
     constexpr int W = rec_words<T>();
+    if constexpr (rec_bytes<T>() == 10) {   // fp64, 10-byte records
+        const char* p = reinterpret_cast<const char*>(rec) + (uint64_t)((uint32_t)i * 10u);
+        const uint32_t sh = (uint32_t)((uintptr_t)p & 2u) * 8u;     // 0 or 16 bits
+#if SPG_NT_REC
+        typedef unsigned u32x3 __attribute__((ext_vector_type(3)));
+        const u32x3 y = __builtin_nontemporal_load(reinterpret_cast<const u32x3*>(p - ((uintptr_t)p & 2u)));
+        const uint3 x = make_uint3(y.x, y.y, y.z);
+#else
+        const uint3 x = *reinterpret_cast<const uint3*>(p - ((uintptr_t)p & 2u));
+#endif
+        const uint32_t lo = __builtin_amdgcn_alignbit(x.y, x.x, sh);
+        const uint32_t hi = __builtin_amdgcn_alignbit(x.z, x.y, sh);
+        v = __hiloint2double((int)hi, (int)lo);
+        lc = (int)((x.z >> sh) & 0xffffu);
+        return;
+    }
     const uint32_t* __restrict__ q =
         reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(rec) + (uint64_t)((uint32_t)i * (uint32_t)(4 * W)));
     if constexpr (W == 2) {          // f32
@@ -134,6 +167,15 @@ __device__ __forceinline__ void load_rec(const uint32_t* __restrict__ rec, IP i,
 
 template <typename T>
 __device__ __forceinline__ void store_rec(uint32_t* __restrict__ rec, int64_t i, int lc, T v) {
+    if constexpr (rec_bytes<T>() == 10) {   // five 2-byte stores (a record is 2-byte aligned)
+        uint16_t* q = reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(rec) + i * 10);
+        uint64_t b;
+        __builtin_memcpy(&b, &v, 8);
+#pragma unroll
+        for (int h = 0; h < 4; ++h) q[h] = (uint16_t)(b >> (16 * h));
+        q[4] = (uint16_t)lc;
+        return;
+    }
     constexpr int W = rec_words<T>();
     uint32_t* q = rec + i * W;
     __builtin_memcpy(q, &v, sizeof(T));
@@ -143,15 +185,15 @@ __device__ __forceinline__ void store_rec(uint32_t* __restrict__ rec, int64_t i,
 // Sentinel records after B's nnz records: the lean tile kernels point every product slot past
 // the end of a batch at them instead of masking the slot (no compare / select per chunk).
 // Regions 0 and 1 (dense tiles of 1024 / 2048 columns): columns 1024 / 2048 + (i % 32),
-// accumulator slots nobody reads; region 2 (sparse tiles): columns >= 65536, outside every
-// window.  Value 0.
+// accumulator slots nobody reads; region 2 (sparse tiles, <= 8192 columns): columns
+// 65472 + (i % 64), outside every window (and within the 10-byte records' u16).  Value 0.
 constexpr int SENT_N = 512;        // records per region: a step never runs more than 512 slots past its batch
 constexpr int SENT_REGIONS = 3;
 constexpr int DN_DUMMY = 32;       // accumulator slots past a dense tile: the sentinel records add into them
 constexpr int DN_TW_MAX = 2048;    // widest dense tile (fp64: 2048-slot accumulator)
 __device__ __forceinline__ int sentinel_col(int i) {
     const int r = i / SENT_N, x = i % SENT_N;
-    return r == 0 ? 1024 + (x & (DN_DUMMY - 1)) : r == 1 ? 2048 + (x & (DN_DUMMY - 1)) : 65536 + (x & 63);
+    return r == 0 ? 1024 + (x & (DN_DUMMY - 1)) : r == 1 ? 2048 + (x & (DN_DUMMY - 1)) : 0xffc0 + (x & 63);
 }
 __host__ __device__ constexpr int sentinel_region(int dense_tw) { return dense_tw == 1024 ? 0 : dense_tw == 2048 ? 1 : 2; }
 

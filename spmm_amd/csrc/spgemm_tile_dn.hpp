@@ -68,24 +68,31 @@ __global__ __launch_bounds__(WAVE) void k_lds_order_check(const double* __restri
 #ifndef SPG_NT_C
 #define SPG_NT_C 1
 #endif
+// SPG_NT_A: non-temporal A-row reads in the dense-tile kernel (1, default: config 4 19.8 -> 19.4 ms;
+// the sparse-tile kernel keeps plain loads, config 5 98.7 -> 100.5 ms with them; 2: both)
 #ifndef SPG_NT_A
-#define SPG_NT_A 0
+#define SPG_NT_A 1
 #endif
+// SPG_NT_C 2: relaxed agent-scope atomic stores, which gfx950 emits as `sc1` stores: the line
+// leaves the XCD's L2 instead of staying there (MI355X_MICROARCH.md, stores of each flavour).
 template <typename T> __device__ __forceinline__ void st_c(T* p, T v) {
-    if constexpr (SPG_NT_C != 0 && (sizeof(T) == 4 || sizeof(T) == 8)) __builtin_nontemporal_store(v, p);
+    if constexpr (SPG_NT_C == 2 && (sizeof(T) == 4 || sizeof(T) == 8))
+        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else if constexpr (SPG_NT_C != 0 && (sizeof(T) == 4 || sizeof(T) == 8)) __builtin_nontemporal_store(v, p);
     else *p = v;
 }
 template <typename R> __device__ __forceinline__ void st_c(cplx<R>* p, cplx<R> v) {
     st_c(&p->re, v.re);
     st_c(&p->im, v.im);
 }
-template <typename T> __device__ __forceinline__ T ld_a(const T* p) {
-    if constexpr (SPG_NT_A != 0 && (sizeof(T) == 4 || sizeof(T) == 8)) return __builtin_nontemporal_load(p);
+template <bool NT = (SPG_NT_A != 0), typename T> __device__ __forceinline__ T ld_a(const T* p) {
+    if constexpr (NT && (sizeof(T) == 4 || sizeof(T) == 8)) return __builtin_nontemporal_load(p);
     else return *p;
 }
-template <typename R> __device__ __forceinline__ cplx<R> ld_a(const cplx<R>* p) {
-    return cplx<R>(ld_a(&p->re), ld_a(&p->im));
+template <bool NT = (SPG_NT_A != 0), typename R> __device__ __forceinline__ cplx<R> ld_a(const cplx<R>* p) {
+    return cplx<R>(ld_a<NT>(&p->re), ld_a<NT>(&p->im));
 }
+constexpr bool SP_NT_A = SPG_NT_A == 2;   // (the sparse-tile kernels)
 
 constexpr int DN_WPB = 2;     // waves per block
 
@@ -179,7 +186,7 @@ __device__ __forceinline__ void dn_walk(L* lp, T* acc, int l, const int32_t* __r
                                         Slot&& slot, Hit&& hit, int32_t (*kq)[NB] = nullptr, int klo = 0,
                                         int khi = 0) {
     constexpr int U = sizeof(T) > 8 ? 4 : 8;     // chunks in flight
-    constexpr uint32_t RB = 4u * (uint32_t)rec_words<T>();   // bytes of one B record
+    constexpr uint32_t RB = (uint32_t)rec_bytes<T>();   // bytes of one B record
     DnEnt<T>* ent = lp->ent;
     uint8_t* mk = lp->mk;
     for (int b = 0; b < nA; b += WAVE) {
@@ -297,7 +304,7 @@ __device__ __forceinline__ void dn_emit(DnLds<T, TWD>& S, int l, int TW, int lo,
                                         int64_t a0, int nA, const int32_t* __restrict__ Aj,
                                         const char* __restrict__ rb, int32_t* __restrict__ crow,
                                         T* __restrict__ xrow, T alpha) {
-    constexpr uint32_t RB = 4u * (uint32_t)rec_words<T>();
+    constexpr uint32_t RB = (uint32_t)rec_bytes<T>();
     wsync();
     // the item's structure, 64 columns at a time: hit[] or (dn_sent) the non -0.0 slots
     // (4 column groups per round: their LDS reads in flight together, TW >= 256)
@@ -354,7 +361,6 @@ __device__ __forceinline__ void dn_emit(DnLds<T, TWD>& S, int l, int TW, int lo,
 #ifndef SPG_SP_WIDE
 #define SPG_SP_WIDE 0
 #endif
-#if SPG_DN_WIDE || SPG_SP_WIDE
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void st_c4(int32_t* p, i32x4 v) {
@@ -365,7 +371,6 @@ __device__ __forceinline__ void st_c2(double* p, f64x2 v) {
     if constexpr (SPG_NT_C != 0) __builtin_nontemporal_store(v, reinterpret_cast<f64x2*>(p));
     else *reinterpret_cast<f64x2*>(p) = v;
 }
-#endif
 #if SPG_DN_WIDE
 
 // The item's output with 16-byte stores (fp64 dense tiles, dn_sent): the slots that left -0.0
@@ -681,8 +686,8 @@ void k_tile_sp(
                 kq[q] = -1;
                 aq[q] = (T)0;
                 if (q * WAVE + l < nA) {
-                    kq[q] = ld_a(Aj + a0 + q * WAVE + l);
-                    aq[q] = ld_a(Ax + a0 + q * WAVE + l);
+                    kq[q] = ld_a<SP_NT_A>(Aj + a0 + q * WAVE + l);
+                    aq[q] = ld_a<SP_NT_A>(Ax + a0 + q * WAVE + l);
                 }
             }
 #pragma unroll
@@ -894,8 +899,8 @@ __global__ __launch_bounds__((sp_ph_wpb<T, SP_CAP>() * WAVE)) void k_tile_sp_ph(
             kq[q] = -1;
             aq[q] = (T)0;
             if (q * WAVE + l < nA) {
-                kq[q] = ld_a(Aj + a0 + q * WAVE + l);
-                aq[q] = ld_a(Ax + a0 + q * WAVE + l);
+                kq[q] = ld_a<SP_NT_A>(Aj + a0 + q * WAVE + l);
+                aq[q] = ld_a<SP_NT_A>(Ax + a0 + q * WAVE + l);
             }
         }
 #pragma unroll
