@@ -271,6 +271,17 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t nb) {
     const uint32_t b = blockIdx.x;
     return (b & 7u) * (nb >> 3) + (b >> 3);
 }
+// Numeric tile kernels' item map.  SPG_ITEM_MAP 1: xcd_block (every XCD its own run of tiles);
+// 0: dispatch order, so the eight XCDs work through the same tile's rows together -- each L2
+// still sees the whole slice, but the Infinity Cache holds one slice instead of eight (config 5:
+// 8 x 21.5 MB of slices against a C stream of ~190 MB between two uses of a record line).
+#ifndef SPG_ITEM_MAP
+#define SPG_ITEM_MAP 1
+#endif
+__device__ __forceinline__ uint32_t item_block(uint32_t nb) {
+    if constexpr (SPG_ITEM_MAP != 0) return xcd_block(nb);
+    else return blockIdx.x;
+}
 
 constexpr int SYM_NWMAX = 2048;   // symbolic bitmap words: 65536 columns
 
@@ -420,6 +431,139 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile_sym(
         }
         // entry count of each numeric tile: lane t sums tile t's words (rotated start: no
         // two lanes read one bank together)
+        for (int t = l; t < t1 - t0; t += WAVE) {
+            int c = 0;
+            for (int j = 0; j < nw; ++j) c += __popc(S.bits[t * nw + ((j + t) & (nw - 1))]);
+            item_cnt[(row - row0) * G + t0 + t] = c;
+        }
+    }
+}
+
+// Symbolic pass of the tile path, walking 16-byte WORDS of B's 16-bit columns (k_bj16) instead
+// of products (round 4).  The bitmap OR is order-free, so a wave needs no (jj, kk) product order:
+// each A entry's segment [beg, beg + cnt) of its B row inside the symbolic tile covers
+// ceil(((beg & 7) + cnt) / 8) aligned words; the words of a batch of 64 entries are flattened
+// (DPP scan of the word counts, transposed markers + max-scan for the lane -> entry map, as
+// k_tile_sym does for products) and every lane loads ONE word -- 8 columns -- per chunk of 64
+// words, masks the columns outside its entry's segment and sets their bits.  A chunk thus moves
+// up to 512 columns with one 16-byte load per lane where k_tile_sym moves 64 with one 2-byte load
+// per lane (config 5's 65-column segments: ~9 words each, 89 % of the slots used).
+struct __attribute__((aligned(16))) Sym8Ent {
+    uint32_t w0;     // first word (index into the uint4 view of Bj16)
+    uint32_t woff;   // flattened offset of the entry's first word
+    uint32_t wlen;   // words
+    uint32_t lohi;   // (beg & 7) | (((beg + cnt - 1) & 7) + 1) << 8: valid halves of the first / last word
+};
+struct Sym8Lds {
+    uint32_t bits[SYM_NWMAX];
+    Sym8Ent ent[WAVE];
+    uint8_t mk[TILE_MK];
+};
+template <typename IP>
+__global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile_sym8(
+    int64_t row0, int64_t nrows, int tws, int G, int twss, const IP* __restrict__ Ap,
+    const int32_t* __restrict__ Aj, const IP* __restrict__ Bp, const uint16_t* __restrict__ Bj16,
+    const uint32_t* __restrict__ sidx, uint32_t* __restrict__ bitmap, int64_t* __restrict__ item_cnt) {
+    constexpr int U = 8;   // chunks of 64 words in flight
+    __shared__ __attribute__((aligned(16))) Sym8Lds lds[TILE_WPB];
+    const int l = lane_id();
+    const int wv = uniform((int)(threadIdx.x >> 6));
+    Sym8Lds& S = lds[wv];
+    const uint4* __restrict__ W = reinterpret_cast<const uint4*>(Bj16);
+    const int nw = (1 << tws) >> 5;           // bitmap words of a numeric tile
+    const int R = 1 << (twss - tws);          // numeric tiles per symbolic tile
+    const int Gs = (G + R - 1) / R;           // symbolic tiles per row
+    const uint32_t tasks = (uint32_t)(nrows * Gs);
+    const uint32_t stride = gridDim.x * TILE_WPB;
+    for (uint32_t task = xcd_block(gridDim.x) * TILE_WPB + wv; task < tasks; task += stride) {
+        const int64_t row = row0 + (int64_t)(task / (uint32_t)Gs);
+        const int gs = (int)(task % (uint32_t)Gs);
+        const int t0 = gs * R, t1 = min(G, t0 + R);
+        const int lo16 = (t0 << tws) & 0xffff;
+        const int nws = (t1 - t0) * nw;
+        const int64_t a0 = Ap[row];
+        const int nA = (int)(Ap[row + 1] - a0);
+        if (nA <= 0) {
+            for (int t = t0 + l; t < t1; t += WAVE) item_cnt[(row - row0) * G + t] = 0;
+            continue;
+        }
+        wsync();
+        for (int w = l; w < nws; w += WAVE) S.bits[w] = 0u;
+        for (int b = 0; b < nA; b += WAVE) {
+            int wlen = 0;
+            Sym8Ent e{0u, 0u, 0u, 0u};
+            int64_t bg = 0;
+            int cnt = 0;
+            if (b + l < nA) {
+                const int32_t k = Aj[a0 + b + l];
+                const IP rb = Bp[k];
+                if (Gs == 1) {
+                    cnt = (int)(Bp[k + 1] - rb);
+                    bg = (int64_t)rb;
+                } else {
+                    const uint32_t* sk = sidx + (int64_t)k * (Gs + 1);
+                    const uint32_t s0 = sk[gs];
+                    cnt = (int)(sk[gs + 1] - s0);
+                    bg = (int64_t)rb + s0;
+                }
+            }
+            if (cnt > 0) {
+                wlen = (int)(((bg + cnt + 7) >> 3) - (bg >> 3));
+                e.w0 = (uint32_t)(bg >> 3);
+                e.lohi = (uint32_t)(bg & 7) | ((uint32_t)(((bg + cnt - 1) & 7) + 1) << 8);
+            }
+            const int incl = wave_incl_sum_dpp(wlen);
+            const int woff = incl - wlen;
+            const int Wb = readlane_i(incl, WAVE - 1);
+            wsync();
+            e.woff = (uint32_t)woff;
+            e.wlen = (uint32_t)wlen;
+            S.ent[l] = e;
+            wsync();
+            unsigned carry = 0u;
+            for (int gb = 0; gb < Wb; gb += TILE_MK) {
+                group_markers(S, l, wlen, woff, gb);
+                const int nchg = min(TILE_MK, Wb - gb);
+                const uint4 mrow = reinterpret_cast<const uint4*>(S.mk)[l];
+                for (int c0 = 0; c0 < nchg; c0 += U * WAVE) {
+                    const uint64_t mb = marker_bytes(mrow, c0 >> 6);
+                    uint4 w[U];
+                    uint32_t lo[U], hi[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        lo[u] = 8u;   // (no valid column: slots past the group's words)
+                        hi[u] = 0u;
+                        w[u] = make_uint4(0u, 0u, 0u, 0u);
+                        const int cc = c0 + u * WAVE;
+                        if (cc < nchg) {
+                            const unsigned sp = max(wave_incl_umax_dpp((unsigned)(mb >> (8 * u)) & 0xffu), carry);
+                            carry = (unsigned)readlane_i((int)sp, WAVE - 1);
+                            const int t = gb + cc + l;
+                            if (t < Wb) {
+                                const Sym8Ent x = S.ent[(int)sp - 1];
+                                const uint32_t wi = (uint32_t)t - x.woff;
+                                lo[u] = wi == 0u ? (x.lohi & 0xffu) : 0u;
+                                hi[u] = wi + 1u == x.wlen ? (x.lohi >> 8) : 8u;
+                                w[u] = W[x.w0 + wi];
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const uint32_t ww[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
+#pragma unroll
+                        for (int h = 0; h < 8; ++h)
+                            if ((uint32_t)h >= lo[u] && (uint32_t)h < hi[u])
+                                set_bit(S.bits, (int)((ww[h >> 1] >> (16 * (h & 1))) & 0xffffu) - lo16);
+                    }
+                }
+            }
+        }
+        wsync();
+        if (bitmap) {   // (dense numeric tiles take their structure from the accumulation)
+            uint32_t* __restrict__ out = bitmap + ((row - row0) * G + t0) * (int64_t)nw;
+            for (int w = l; w < nws; w += WAVE) out[w] = S.bits[w];
+        }
         for (int t = l; t < t1 - t0; t += WAVE) {
             int c = 0;
             for (int j = 0; j < nw; ++j) c += __popc(S.bits[t * nw + ((j + t) & (nw - 1))]);

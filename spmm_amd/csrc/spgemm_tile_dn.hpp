@@ -497,7 +497,7 @@ __global__ __launch_bounds__(dn_wpb<PH>() * WAVE) void k_tile_dn(
     const uint32_t items = (uint32_t)(nrows * G);   // host keeps rows*G < 2^31
     // (base is block-uniform: with PH > 1 every wave of the block meets every barrier, items
     // or not)
-    for (uint32_t base = xcd_block(gridDim.x) * WPB; base < items; base += gridDim.x * WPB) {
+    for (uint32_t base = item_block(gridDim.x) * WPB; base < items; base += gridDim.x * WPB) {
         const uint32_t it = base + wv;
         bool live = it < items;
         int g = 0, nnz = 0, nA = 0;
@@ -644,7 +644,7 @@ void k_tile_sp(
     const char* __restrict__ rb = reinterpret_cast<const char*>(brec);
     const uint32_t items = (uint32_t)(nrows * G);
     const bool one = alpha == (T)1;
-    for (uint32_t it = xcd_block(gridDim.x) * SP_WPB + wv; it < items; it += gridDim.x * SP_WPB) {
+    for (uint32_t it = item_block(gridDim.x) * SP_WPB + wv; it < items; it += gridDim.x * SP_WPB) {
         const int g = (int)(it / (uint32_t)nrows);
         const int64_t row = row0 + (int64_t)(it - (uint32_t)g * (uint32_t)nrows);
         const int64_t item = (row - row0) * G + g;
@@ -860,7 +860,7 @@ __global__ __launch_bounds__((sp_ph_wpb<T, SP_CAP>() * WAVE)) void k_tile_sp_ph(
     const char* __restrict__ rb = reinterpret_cast<const char*>(brec);
     const uint32_t items = (uint32_t)(nrows * G);
     const bool one = alpha == (T)1;
-    for (uint32_t base = xcd_block(gridDim.x) * WPB; base < items; base += gridDim.x * WPB) {
+    for (uint32_t base = item_block(gridDim.x) * WPB; base < items; base += gridDim.x * WPB) {
         const uint32_t it = base + wv;
         bool live = it < items;
         int g = 0, nA = 0;
