@@ -2,7 +2,8 @@
 # Profile collection on the GPU box (run through gpurun from the repo root).
 #   1. bench.py (BENCH_ARGS) -> gpurun_out/bench_<tag>.json
 #   2. rocprofv3 --kernel-trace --stats of the same command -> gpurun_out/prof_<tag>/trace_*
-#   3. two separate PMC passes (FETCH_SIZE, WRITE_SIZE: they do not fit one TCC pass)
+#   3. three separate PMC passes (FETCH_SIZE, WRITE_SIZE, TCC_HIT + TCC_MISS: they do not fit
+#      one TCC pass)
 #   4. summary + pmc_traffic.json entry (stamped with the library's build id)
 # Every GPU step has its own time limit and the steps are chained with &&.
 set -euo pipefail
@@ -21,6 +22,8 @@ timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$P" -o pm
     -- python3 bench.py $ARGS --steps 3 --warmup 1 --cpu-seconds 0 > "$P/fetch.log" 2>&1
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$P" -o pmc_write \
     -- python3 bench.py $ARGS --steps 3 --warmup 1 --cpu-seconds 0 > "$P/write.log" 2>&1
+timeout -s KILL 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$P" -o pmc_hit \
+    -- python3 bench.py $ARGS --steps 3 --warmup 1 --cpu-seconds 0 > "$P/hit.log" 2>&1
 python3 profiles/summarize.py "$P" > "$OUT/summary_$TAG.txt"
 python3 profiles/pmc_to_json.py "$P" "$PMC_KEY" "$PMC_KERNEL" "$OUT/pmc_traffic.json"
 echo "collect done ($TAG)"

@@ -7,8 +7,8 @@ MI355X_MICROARCH.md "HBM [CDNA4]":
   write = WRITE_SIZE (KiB) x 1024
 FETCH_SIZE counts L2 misses to the fabric, Infinity-Cache hits included, so for inputs that
 stay resident in the 256 MiB Infinity Cache it is an upper bound on HBM reads.  The x2
-correction is calibrated for 16-B/lane streaming reads only: the gathers of B here are
-narrower, so the corrected read figure is an upper bound too (raw values are kept).
+correction holds for the tile kernels' gathers as well (round 4 calibration,
+abtest/gather_probe.sh: every fabric read request is 128 B).  A third pass adds the L2 hit rate.
 
 Each entry is stamped with the build id of the library it was measured on
 (spmm_amd._lib.build_id(): SHA-256 of libmi355_spgemm.so); bench.py reports a traffic figure
@@ -50,6 +50,8 @@ def main():
     write, nw = per_launch(d, "WRITE_SIZE", rx)
     if fetch is None or write is None:
         raise SystemExit(f"no FETCH_SIZE/WRITE_SIZE rows for /{pat}/ under {d}")
+    hit, _ = per_launch(d, "TCC_HIT_sum", rx)
+    miss, _ = per_launch(d, "TCC_MISS_sum", rx)
     rd = fetch * 1024 * 2
     wr = write * 1024
     db = json.load(open(path)) if os.path.exists(path) else {}
@@ -57,7 +59,11 @@ def main():
                "fetch_size_kib": round(fetch, 1), "write_size_kib": round(write, 1),
                "read_bytes_per_launch": int(rd), "write_bytes_per_launch": int(wr),
                "hbm_bytes_per_launch": int(rd + wr),
-               "note": "FETCH_SIZE x2 (gfx950) + WRITE_SIZE; Infinity-Cache hits included",
+               "l2_hit_rate": round(hit / (hit + miss), 4) if hit is not None and miss is not None and hit + miss else None,
+               "note": ("FETCH_SIZE x2 + WRITE_SIZE; Infinity-Cache hits included.  The x2 is exact for these "
+                        "gathers too: every fabric read request of the 12-/10-byte record gathers is a 128-byte "
+                        "request tallied at 64 B (TCC_EA0_RDREQ_128B_sum = TCC_EA0_RDREQ_sum, "
+                        "abtest/gather_probe.sh, profiles/r04_gather_probe.txt)"),
                "build_id": build_id(), "source_id": source_id()}
     json.dump(db, open(path, "w"), indent=1, sort_keys=True)
     print(json.dumps({key: db[key]}))
