@@ -60,7 +60,7 @@ template <int U, int RB>
 __global__ __launch_bounds__(WPB * 64) void k_gather(const uint32_t* __restrict__ rec, int64_t slice_recs, int L,
                                                      int chunks, int store, int32_t* __restrict__ cj,
                                                      double* __restrict__ cx, int64_t out_per_wave,
-                                                     double* sink) {
+                                                     double* sink, int align) {
     const int l = threadIdx.x & 63;
     const uint32_t wave = blockIdx.x * WPB + (threadIdx.x >> 6);
     const int64_t base = (int64_t)(blockIdx.x & 7) * slice_recs;
@@ -77,13 +77,16 @@ __global__ __launch_bounds__(WPB * 64) void k_gather(const uint32_t* __restrict_
         for (int u = 0; u < U; ++u) {
             const uint32_t t = (uint32_t)(c0 + u) * 64u + (uint32_t)l;
             const uint32_t seg = t / (uint32_t)L, kk = t - seg * (uint32_t)L;
-            const uint32_t start = mix(seg * 2654435761u ^ wave * 40503u) % span;
+            const uint32_t r = mix(seg * 2654435761u ^ wave * 40503u);
+            // align: every segment starts at a 128-byte line (the slice holds slice_recs*RB/128 lines)
+            const uint64_t sb = align ? (uint64_t)(r % (uint32_t)((slice_recs * RB) / 128 - 2)) * 128u
+                                      : (uint64_t)(r % span) * RB;
             if constexpr (RB == 12) {
-                const uint3 x = *reinterpret_cast<const uint3*>(rb + (uint64_t)(start + kk) * 12u);
+                const uint3 x = *reinterpret_cast<const uint3*>(rb + sb + (uint64_t)kk * 12u);
                 v[u] = __hiloint2double((int)x.y, (int)x.x);
                 col[u] = (int)x.z;
             } else {
-                const uint4 x = *reinterpret_cast<const uint4*>(rb + (uint64_t)(start + kk) * 16u);
+                const uint4 x = *reinterpret_cast<const uint4*>(rb + sb + (uint64_t)kk * 16u);
                 v[u] = __hiloint2double((int)x.y, (int)x.x);
                 col[u] = (int)x.z;
             }
@@ -137,6 +140,7 @@ int main(int argc, char** argv) {
     const int wpc = argc > 5 ? std::atoi(argv[5]) : 8;       // waves per CU (one generation)
     const int U = argc > 6 ? std::atoi(argv[6]) : 8;         // loads in flight per wave (8 or 16)
     const int RB = argc > 7 ? std::atoi(argv[7]) : 12;       // record bytes (12 or 16)
+    const int align = argc > 8 ? std::atoi(argv[8]) : 0;      // segments start at 128-byte lines
     const int64_t total_chunks = (int64_t)256 * 32 * 4096;   // 2^25 wave instructions = 2^31 products
     const int chunks = (int)(total_chunks / (256 * wpc));
     const int64_t slice = (int64_t)(smb * 1048576.0) / RB;
@@ -167,7 +171,7 @@ int main(int argc, char** argv) {
         CK(hipEventRecord(a));
         auto go = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(blocks), dim3(WPB * 64), 0, 0, rec, slice, L, chunks, store, cj, cx,
-                               out_per_wave, sink);
+                               out_per_wave, sink, align);
         };
         if (U == 16) { if (RB == 16) go(k_gather<16, 16>); else go(k_gather<16, 12>); }
         else { if (RB == 16) go(k_gather<8, 16>); else go(k_gather<8, 12>); }
@@ -181,10 +185,10 @@ int main(int argc, char** argv) {
     const double products = (double)waves * chunks * 64;
     const double rbytes = (double)RB * products;
     const double wbytes = store ? 12.0 * (double)waves * out_per_wave : 0.0;
-    std::printf("{\"mode\": \"gather\", \"slice_MB\": %.2f, \"L\": %d, \"store\": %d, \"waves_per_cu\": %d, \"U\": %d, \"rec_bytes\": %d, \"launches\": %d, "
+    std::printf("{\"mode\": \"gather\", \"slice_MB\": %.2f, \"L\": %d, \"store\": %d, \"waves_per_cu\": %d, \"U\": %d, \"rec_bytes\": %d, \"align\": %d, \"launches\": %d, "
                 "\"products\": %.0f, \"record_bytes_per_launch\": %.0f, \"store_bytes_per_launch\": %.0f, "
                 "\"best_ms\": %.4f, \"record_GBps\": %.1f, \"total_GBps\": %.1f}\n",
-                smb, L, store, wpc, U, RB, reps, products, rbytes, wbytes, best, rbytes / (best * 1e-3) / 1e9,
+                smb, L, store, wpc, U, RB, align, reps, products, rbytes, wbytes, best, rbytes / (best * 1e-3) / 1e9,
                 (rbytes + wbytes) / (best * 1e-3) / 1e9);
     return 0;
 }

@@ -179,14 +179,6 @@ inline bool row_kernel_enabled() {
 #define SPG_TILE_TWS 0
 #endif
 //   SPG_TILE_LEAN   0 keeps the owner-round k_tile on dense tiles (A/B against k_tile_dn)
-//   SPG_DN_PH       k phases per dense 2048-column item (k_tile_dn<.., PH>; 1 = unphased)
-#ifndef SPG_DN_PH
-#define SPG_DN_PH 1
-#endif
-//   SPG_SP_PH       k phases per sparse 8192-column item (k_tile_sp_ph<.., PH>; 1 = k_tile_sp)
-#ifndef SPG_SP_PH
-#define SPG_SP_PH 1
-#endif
 //   SPG_SYM8        symbolic tiles by the word-flattened walk (k_tile_sym8, default) instead of
 //                   k_tile_sym (config 5: 20.1 -> 12.1 ms)
 #ifndef SPG_SYM8
@@ -1018,17 +1010,6 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
             if (!dense && p.lean && SPG_SP_LEAN) {   // sparse tiles, ordered LDS adds
                 auto sp = [&](auto capc) {
                     constexpr int CAP = decltype(capc)::value;
-                    // k-phased items (SPG_SP_PH, A/B builds; fp64 8192-column tiles)
-                    constexpr int PH = (std::is_same<T, double>::value && CAP == 2048) ? SPG_SP_PH : 1;
-                    if constexpr (PH > 1) {
-                        constexpr int W = sp_ph_wpb<T, CAP>();
-                        const unsigned grid = std::min<unsigned>(tile_grid(n * p.G, W), (unsigned)(h->cus + 7) / 8 * 8);
-                        hipExtLaunchKernelGGL((k_tile_sp_ph<T, IP, CAP, PH>), dim3(grid), dim3(W * WAVE), 0, h->stream,
-                                              kt.a, kt.b, 0, r0, n, p.tws, p.G, Ap, Aj, Ax, p.B.rows,
-                                              (const uint32_t*)p.brec, (const int32_t*)p.tptr, (const uint32_t*)p.bitmap,
-                                              (const int64_t*)tile_chunk_items(p, c), cj, cx, alpha, sent(2));
-                        return;
-                    }
                     hipExtLaunchKernelGGL((k_tile_sp<T, IP, CAP>), dim3(tile_grid(n * p.G, SP_WPB)), dim3(SP_WPB * WAVE),
                                           0, h->stream, kt.a, kt.b, 0, r0, n, p.tws, p.G, Ap, Aj, Ax, p.B.rows,
                                           (const uint32_t*)p.brec, (const int32_t*)p.tptr, (const uint32_t*)p.bitmap,
@@ -1047,13 +1028,7 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
             if (dense && p.lean) {   // ordered LDS adds (spgemm_tile_dn.hpp)
                 auto dn = [&](auto twd) {
                     constexpr int TWD = decltype(twd)::value;
-                    // k-phased items (SPG_DN_PH, A/B builds; fp64 2048-column tiles)
-                    constexpr int PH = (std::is_same<T, double>::value && TWD == 2048) ? SPG_DN_PH : 1;
-                    constexpr int W = dn_wpb<PH>();
-                    // (phased: one 8-wave block per CU, persistent, so a CU's items stay in step)
-                    const unsigned grid = PH > 1 ? std::min<unsigned>(tile_grid(n * p.G, W), (unsigned)(h->cus + 7) / 8 * 8)
-                                                 : tile_grid(n * p.G, W);
-                    hipExtLaunchKernelGGL((k_tile_dn<T, IP, TWD, PH>), dim3(grid), dim3(W * WAVE),
+                    hipExtLaunchKernelGGL((k_tile_dn<T, IP, TWD>), dim3(tile_grid(n * p.G, DN_WPB)), dim3(DN_WPB * WAVE),
                                           0, h->stream, kt.a, kt.b, 0, r0, n, p.tws, p.G, Ap, Aj, Ax, p.B.rows,
                                           (const uint32_t*)p.brec, (const int32_t*)p.tptr,
                                           (const int64_t*)tile_chunk_items(p, c), cj, cx, alpha,

@@ -117,10 +117,6 @@ template <typename T> constexpr int rec_words() { return 1 + (int)(sizeof(T) / 4
 #ifndef SPG_REC10
 #define SPG_REC10 1
 #endif
-// SPG_NT_REC (A/B builds): the 10-byte record gathers as non-temporal loads
-#ifndef SPG_NT_REC
-#define SPG_NT_REC 0
-#endif
 template <typename T> constexpr int rec_bytes() {
     return (SPG_REC10 && std::is_same<T, double>::value) ? 10 : 4 * rec_words<T>();
 }
@@ -131,13 +127,7 @@ __device__ __forceinline__ void load_rec(const uint32_t* __restrict__ rec, IP i,
     if constexpr (rec_bytes<T>() == 10) {   // fp64, 10-byte records
         const char* p = reinterpret_cast<const char*>(rec) + (uint64_t)((uint32_t)i * 10u);
         const uint32_t sh = (uint32_t)((uintptr_t)p & 2u) * 8u;     // 0 or 16 bits
-#if SPG_NT_REC
-        typedef unsigned u32x3 __attribute__((ext_vector_type(3)));
-        const u32x3 y = __builtin_nontemporal_load(reinterpret_cast<const u32x3*>(p - ((uintptr_t)p & 2u)));
-        const uint3 x = make_uint3(y.x, y.y, y.z);
-#else
-        const uint3 x = *reinterpret_cast<const uint3*>(p - ((uintptr_t)p & 2u));
-#endif
+const uint3 x = *reinterpret_cast<const uint3*>(p - ((uintptr_t)p & 2u));
         const uint32_t lo = __builtin_amdgcn_alignbit(x.y, x.x, sh);
         const uint32_t hi = __builtin_amdgcn_alignbit(x.z, x.y, sh);
         v = __hiloint2double((int)hi, (int)lo);
@@ -271,18 +261,6 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t nb) {
     const uint32_t b = blockIdx.x;
     return (b & 7u) * (nb >> 3) + (b >> 3);
 }
-// Numeric tile kernels' item map.  SPG_ITEM_MAP 1: xcd_block (every XCD its own run of tiles);
-// 0: dispatch order, so the eight XCDs work through the same tile's rows together -- each L2
-// still sees the whole slice, but the Infinity Cache holds one slice instead of eight (config 5:
-// 8 x 21.5 MB of slices against a C stream of ~190 MB between two uses of a record line).
-#ifndef SPG_ITEM_MAP
-#define SPG_ITEM_MAP 1
-#endif
-__device__ __forceinline__ uint32_t item_block(uint32_t nb) {
-    if constexpr (SPG_ITEM_MAP != 0) return xcd_block(nb);
-    else return blockIdx.x;
-}
-
 constexpr int SYM_NWMAX = 2048;   // symbolic bitmap words: 65536 columns
 
 template <typename IP> struct SymLds {

@@ -73,12 +73,8 @@ __global__ __launch_bounds__(WAVE) void k_lds_order_check(const double* __restri
 #ifndef SPG_NT_A
 #define SPG_NT_A 1
 #endif
-// SPG_NT_C 2: relaxed agent-scope atomic stores, which gfx950 emits as `sc1` stores: the line
-// leaves the XCD's L2 instead of staying there (MI355X_MICROARCH.md, stores of each flavour).
 template <typename T> __device__ __forceinline__ void st_c(T* p, T v) {
-    if constexpr (SPG_NT_C == 2 && (sizeof(T) == 4 || sizeof(T) == 8))
-        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else if constexpr (SPG_NT_C != 0 && (sizeof(T) == 4 || sizeof(T) == 8)) __builtin_nontemporal_store(v, p);
+    if constexpr (SPG_NT_C != 0 && (sizeof(T) == 4 || sizeof(T) == 8)) __builtin_nontemporal_store(v, p);
     else *p = v;
 }
 template <typename R> __device__ __forceinline__ void st_c(cplx<R>* p, cplx<R> v) {
@@ -135,19 +131,10 @@ template <typename T, int TWD, bool HIT = !dn_sent<T>()> struct DnLds {
 };
 // (dn_sent, TWD 1024: 10,000 bytes per wave -- 8 two-wave blocks, 16 waves, fit a CU's 160 KB;
 // TWD 2048: 18,192 bytes, 8 waves)
-// SPG_DN_WIDE: the output leaves in 16-byte stores (dn_emit_wide): the item's entries are first
-// compacted in LDS (values in place in acc, u16 columns in cols), a quarter of the store
-// instructions of one 4-byte and one 8-byte store per entry.
-#ifndef SPG_DN_WIDE
-#define SPG_DN_WIDE 0
-#endif
 template <typename T, int TWD> struct DnLds<T, TWD, false> {
     T acc[TWD + DN_DUMMY];
     DnEnt<T> ent[WAVE + 1];
     uint8_t mk[NUM_MK];
-#if SPG_DN_WIDE
-    uint16_t cols[TWD + 8];       // compacted columns (tile-relative), shifted to align the stores
-#endif
 #ifdef SPG_LDS_PAD
     uint8_t pad[SPG_LDS_PAD];   // (A/B builds: occupancy sensitivity)
 #endif
@@ -176,56 +163,41 @@ __device__ __forceinline__ void dn_group_markers(uint8_t* mk, int l, int cnt, in
 // markers; per U chunks the lane -> entry max-scans, one 16-byte table read and one record load
 // per chunk (all in flight), then per chunk in order one multiply and one ds_add_f64 into
 // acc[slot(column)] and hit(slot).  `sent` is the byte offset of the kernel's sentinel region.
-// KR (k-phased items, k_tile_dn<.., PH > 1>): only the A entries whose column k lies in
-// [klo, khi) contribute (`kq` carries the preloaded batches' columns); the entries are sorted, so
-// a phase is a contiguous run of them and batches wholly outside it are skipped.
-template <typename T, int NB, bool KR = false, typename L, typename Slot, typename Hit>
+template <typename T, int NB, typename L, typename Slot, typename Hit>
 __device__ __forceinline__ void dn_walk(L* lp, T* acc, int l, const int32_t* __restrict__ tp, int64_t a0, int nA,
                                         T (&aq)[NB], uint2 (&sq)[NB], const int32_t* __restrict__ Aj,
                                         const T* __restrict__ Ax, const char* __restrict__ rb, uint32_t sent,
-                                        Slot&& slot, Hit&& hit, int32_t (*kq)[NB] = nullptr, int klo = 0,
-                                        int khi = 0) {
+                                        Slot&& slot, Hit&& hit) {
     constexpr int U = sizeof(T) > 8 ? 4 : 8;     // chunks in flight
     constexpr uint32_t RB = (uint32_t)rec_bytes<T>();   // bytes of one B record
     DnEnt<T>* ent = lp->ent;
     uint8_t* mk = lp->mk;
     for (int b = 0; b < nA; b += WAVE) {
         int cnt = 0;
-        uint32_t beg = 0;
+        uint32_t bb = 0;   // byte offset of the entry's segment in the record array
         T av = (T)0;
         if (b < NB * WAVE) {
             // the preloaded batches queue in registers: take the head, shift the rest down
             // (static register indices: a select chain or a dynamic index costs more)
             cnt = (int)(sq[0].y - sq[0].x);
-            beg = sq[0].x;
+            bb = sq[0].x * RB;
             av = aq[0];
-            if constexpr (KR) {
-                if ((*kq)[0] < klo || (*kq)[0] >= khi) cnt = 0;
-#pragma unroll
-                for (int q = 0; q + 1 < NB; ++q) (*kq)[q] = (*kq)[q + 1];
-            }
 #pragma unroll
             for (int q = 0; q + 1 < NB; ++q) {
                 sq[q] = sq[q + 1];
                 aq[q] = aq[q + 1];
             }
         } else if (b + l < nA) {
-            const int32_t k = Aj[a0 + b + l];
-            if (!KR || (k >= klo && k < khi)) {
-                const uint2 se = seg_pair(tp, k);
-                cnt = (int)(se.y - se.x);
-                beg = se.x;
-                av = Ax[a0 + b + l];
-            }
-        }
-        if constexpr (KR) {
-            if (!__ballot(cnt != 0)) continue;   // (a batch outside the phase)
+            const uint2 se = seg_pair(tp, Aj[a0 + b + l]);
+            cnt = (int)(se.y - se.x);
+            bb = se.x * RB;
+            av = Ax[a0 + b + l];
         }
         const int incl = wave_incl_sum_dpp(cnt);
         const int off = incl - cnt;
         const int Pb = readlane_i(incl, WAVE - 1);
         wsync();
-        ent[l].base = beg * RB - (uint32_t)off * RB;   // wraps; base + t*RB is exact
+        ent[l].base = bb - (uint32_t)off * RB;   // wraps; base + t*RB is exact
         ent[l].a = av;
         if (l == 0) {
             ent[WAVE].base = sent - (uint32_t)Pb * RB;   // products Pb.. read sentinel records
@@ -358,82 +330,6 @@ __device__ __forceinline__ void dn_emit(DnLds<T, TWD>& S, int l, int TW, int lo,
     }
 }
 
-#ifndef SPG_SP_WIDE
-#define SPG_SP_WIDE 0
-#endif
-typedef int i32x4 __attribute__((ext_vector_type(4)));
-typedef double f64x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void st_c4(int32_t* p, i32x4 v) {
-    if constexpr (SPG_NT_C != 0) __builtin_nontemporal_store(v, reinterpret_cast<i32x4*>(p));
-    else *reinterpret_cast<i32x4*>(p) = v;
-}
-__device__ __forceinline__ void st_c2(double* p, f64x2 v) {
-    if constexpr (SPG_NT_C != 0) __builtin_nontemporal_store(v, reinterpret_cast<f64x2*>(p));
-    else *reinterpret_cast<f64x2*>(p) = v;
-}
-#if SPG_DN_WIDE
-
-// The item's output with 16-byte stores (fp64 dense tiles, dn_sent): the slots that left -0.0
-// are compacted in column order -- the values in place in acc (an entry's position never
-// exceeds its column, and every 4-group round reads its slots before it writes), the columns
-// as u16 in cols shifted so that the 4-aligned output quads start 8-byte aligned -- then the
-// columns leave as int32 quads and the values as pairs, the unaligned head and tail entry by
-// entry.  Returns the entries found; fewer than nnz (a column reached only by -0.0 products)
-// writes nothing: the caller redoes the item through dn_item's re-walk.
-template <int TWD>
-__device__ __forceinline__ int dn_emit_wide(DnLds<double, TWD>& S, int l, int TW, int lo, int nnz, int64_t obase,
-                                            int32_t* __restrict__ Cj, double* __restrict__ Cx, double alpha) {
-    const int ch = (int)((4 - (obase & 3)) & 3);    // column entries before the first 16-byte boundary
-    const int co = 4 - ch;                          // cols[p + co]: quads at 8-byte aligned LDS offsets
-    const bool one = alpha == 1.0;
-    wsync();
-    int run = 0;
-    for (int k0 = 0; k0 < TW / WAVE; k0 += 4) {
-        double v[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = S.acc[(k0 + e) * WAVE + l];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const bool h = !is_neg_zero(v[e]);
-            const unsigned long long m = __ballot(h);
-            if (h) {
-                const int p = run + lane_rank(m);
-                S.acc[p] = one ? v[e] : mul_rn(alpha, v[e]);
-                S.cols[p + co] = (uint16_t)((k0 + e) * WAVE + l);
-            }
-            run += (int)__popcll(m);
-        }
-    }
-    if (run < nnz || (SPG_TILE_DIAG & 8) != 0) return run;
-    wsync();
-    int32_t* __restrict__ crow = Cj + obase;
-    double* __restrict__ xrow = Cx + obase;
-    // columns: head entries [0, ch), quads [ch + 4i, ch + 4i + 4), tail
-    const int nq = (run - ch) >> 2;
-    if (l < ch && l < run) st_c(crow + l, (int32_t)(lo + S.cols[l + co]));
-    for (int i = l; i < nq; i += WAVE) {
-        const uint2 w = *reinterpret_cast<const uint2*>(&S.cols[4 * i + 4]);
-        const i32x4 c4 = {lo + (int)(w.x & 0xffffu), lo + (int)(w.x >> 16), lo + (int)(w.y & 0xffffu), lo + (int)(w.y >> 16)};
-        st_c4(crow + ch + 4 * i, c4);
-    }
-    {
-        const int t = ch + 4 * nq + l;
-        if (nq >= 0 && l < 4 && t < run && t >= ch) st_c(crow + t, (int32_t)(lo + S.cols[t + co]));
-    }
-    // values: head entry [0, vh), pairs [vh + 2i, vh + 2i + 2), tail
-    const int vh = (int)(obase & 1);
-    const int np = (run - vh) >> 1;
-    if (l < vh && l < run) st_c(xrow + l, S.acc[l]);
-    for (int i = l; i < np; i += WAVE) {
-        const int q = vh + 2 * i;
-        const f64x2 x2 = {S.acc[q], S.acc[q + 1]};
-        st_c2(xrow + q, x2);
-    }
-    if (l == 0 && np >= 0 && vh + 2 * np < run) st_c(xrow + vh + 2 * np, S.acc[vh + 2 * np]);
-    return run;
-}
-#endif
-
 // clear an item's accumulator
 template <typename T, int TWD>
 __device__ __forceinline__ void dn_clear(DnLds<T, TWD>& S, int l, int TW) {
@@ -470,55 +366,34 @@ __device__ __forceinline__ void dn_item(DnLds<T, TWD>& S, int l, int TW, int lo,
 // XCD-aware block map (an XCD works through one tile at a time, so the tile's B slice and
 // segment table stay in its L2), the first NB batches' A entries and tile segments loaded up
 // front.
-//
-// PH > 1 (k-phased items, 8-wave blocks: one block per CU): every item walks its A entries in
-// PH phases of B rows, k in [ph*K/PH, (ph+1)*K/PH), and the block's waves meet at a barrier
-// after every phase.  The wave's accumulator carries the item across its phases and the
-// entries stay in (jj, kk) order inside and across phases, so the sums are exactly those of
-// PH = 1.  What changes is locality: a CU's waves gather from one 1/PH part of the tile's B
-// slice at a time (config 4's 2048-column slice is 8 MB against the XCD's 4 MB L2; at
-// 1/4 of it the gathers hit L2, abtest/gather_probe).
-template <int PH> constexpr int dn_wpb() { return PH > 1 ? 8 : DN_WPB; }
-template <typename T, typename IP, int TWD, int PH = 1>
-__global__ __launch_bounds__(dn_wpb<PH>() * WAVE) void k_tile_dn(
+template <typename T, typename IP, int TWD>
+__global__ __launch_bounds__(DN_WPB * WAVE) void k_tile_dn(
     int64_t row0, int64_t nrows, int tws, int G, const IP* __restrict__ Ap,
     const int32_t* __restrict__ Aj, const T* __restrict__ Ax, int64_t K,
     const uint32_t* __restrict__ brec, const int32_t* __restrict__ tptr,
     const int64_t* __restrict__ item_off, int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha, uint32_t sent) {
     static_assert(OrderedLdsAdd<T>::value, "ordered LDS add needed");
     constexpr int NB = sizeof(T) > 8 ? 4 : 8;    // A batches preloaded per item
-    constexpr int WPB = dn_wpb<PH>();
-    __shared__ __attribute__((aligned(16))) DnLds<T, TWD> lds[WPB];
+    __shared__ __attribute__((aligned(16))) DnLds<T, TWD> lds[DN_WPB];
     const int l = lane_id();
     const int wv = uniform((int)(threadIdx.x >> 6));
     DnLds<T, TWD>& S = lds[wv];
     const int TW = 1 << tws;
     const char* __restrict__ rb = reinterpret_cast<const char*>(brec);
     const uint32_t items = (uint32_t)(nrows * G);   // host keeps rows*G < 2^31
-    // (base is block-uniform: with PH > 1 every wave of the block meets every barrier, items
-    // or not)
-    for (uint32_t base = item_block(gridDim.x) * WPB; base < items; base += gridDim.x * WPB) {
-        const uint32_t it = base + wv;
-        bool live = it < items;
-        int g = 0, nnz = 0, nA = 0;
-        int64_t row = 0, obase = 0, a0 = 0;
-        if (live) {
-            g = (int)(it / (uint32_t)nrows);
-            row = row0 + (int64_t)(it - (uint32_t)g * (uint32_t)nrows);
-            const int64_t item = (row - row0) * G + g;
-            obase = ld_a(item_off + item);
-            nnz = (int)(ld_a(item_off + item + 1) - obase);
-            live = nnz > 0;                          // (no product reaches this tile)
-        }
-        if (PH == 1 && !live) continue;
+    for (uint32_t it = xcd_block(gridDim.x) * DN_WPB + wv; it < items; it += gridDim.x * DN_WPB) {
+        const int g = (int)(it / (uint32_t)nrows);
+        const int64_t row = row0 + (int64_t)(it - (uint32_t)g * (uint32_t)nrows);
+        const int64_t item = (row - row0) * G + g;
+        const int64_t obase = ld_a(item_off + item);
+        const int nnz = (int)(ld_a(item_off + item + 1) - obase);
+        if (nnz == 0) continue;                      // (no product reaches this tile)
         const int32_t* __restrict__ tp = tptr + (int64_t)g * (K + 1);
+        const int64_t a0 = Ap[row];
+        const int nA = (int)(Ap[row + 1] - a0);
         int32_t kq[NB];
         T aq[NB];
         uint2 sq[NB];
-        if (live) {
-            a0 = Ap[row];
-            nA = (int)(Ap[row + 1] - a0);
-        }
 #pragma unroll
         for (int q = 0; q < NB; ++q) {
             kq[q] = -1;
@@ -530,69 +405,7 @@ __global__ __launch_bounds__(dn_wpb<PH>() * WAVE) void k_tile_dn(
         }
 #pragma unroll
         for (int q = 0; q < NB; ++q) sq[q] = kq[q] >= 0 ? seg_pair(tp, kq[q]) : make_uint2(0u, 0u);
-        if constexpr ((SPG_TILE_DIAG & 64) != 0) {   // timing only: no segment-table lookups
-            const uint32_t s0 = (uint32_t)tp[0], s1 = (uint32_t)tp[K];
-#pragma unroll
-            for (int q = 0; q < NB; ++q) {
-                const uint32_t st = s0 + ((uint32_t)kq[q] * 2654435761u) % max(1u, s1 - s0 - 11u);
-                sq[q] = kq[q] >= 0 ? make_uint2(st, st + 10u) : make_uint2(0u, 0u);
-            }
-        }
-        if constexpr (PH == 1) {
-#if SPG_DN_WIDE
-            if constexpr (std::is_same<T, double>::value) {
-                dn_clear(S, l, TW);
-                int32_t kc[NB];
-                dn_walk<T, NB>(&S, S.acc, l, tp, a0, nA, aq, sq, Aj, Ax, rb, sent, [&](int c) { return c; },
-                               [&](int) {});
-                if (dn_emit_wide<TWD>(S, l, TW, g * TW, nnz, obase, Cj, Cx, alpha) < nnz &&
-                    (SPG_TILE_DIAG & 9) == 0) {
-                    // rare: a column reached only by -0.0 products -- the item again through
-                    // dn_item (its re-walk turns such slots into scipy's +0.0)
-#pragma unroll
-                    for (int q = 0; q < NB; ++q) {
-                        kc[q] = -1;
-                        aq[q] = (T)0;
-                        if (q * WAVE + l < nA) {
-                            kc[q] = Aj[a0 + q * WAVE + l];
-                            aq[q] = Ax[a0 + q * WAVE + l];
-                        }
-                    }
-#pragma unroll
-                    for (int q = 0; q < NB; ++q) sq[q] = kc[q] >= 0 ? seg_pair(tp, kc[q]) : make_uint2(0u, 0u);
-                    dn_item<T, NB, TWD>(S, l, TW, g * TW, nnz, tp, a0, nA, aq, sq, Aj, Ax, rb, sent, Cj + obase,
-                                        Cx + obase, alpha);
-                }
-                continue;
-            }
-#endif
-            dn_item<T, NB, TWD>(S, l, TW, g * TW, nnz, tp, a0, nA, aq, sq, Aj, Ax, rb, sent, Cj + obase, Cx + obase,
-                                alpha);
-        } else {
-            if (live) dn_clear(S, l, TW);
-            for (int ph = 0; ph < PH; ++ph) {
-                if (live) {
-                    const int klo = (int)(K * ph / PH), khi = (int)(K * (ph + 1) / PH);
-                    int32_t kc[NB];
-                    T ac[NB];
-                    uint2 sc[NB];
-#pragma unroll
-                    for (int q = 0; q < NB; ++q) {
-                        kc[q] = kq[q];
-                        ac[q] = aq[q];
-                        sc[q] = sq[q];
-                    }
-                    dn_walk<T, NB, true>(&S, S.acc, l, tp, a0, nA, ac, sc, Aj, Ax, rb, sent,
-                                         [&](int c) { return c; },
-                                         [&](int c) {
-                                             if constexpr (!dn_sent<T>()) S.hit[c] = 1;
-                                         },
-                                         &kc, klo, khi);
-                }
-                __syncthreads();
-            }
-            if (live) dn_emit<T, TWD>(S, l, TW, g * TW, nnz, tp, a0, nA, Aj, rb, Cj + obase, Cx + obase, alpha);
-        }
+        dn_item<T, NB, TWD>(S, l, TW, g * TW, nnz, tp, a0, nA, aq, sq, Aj, Ax, rb, sent, Cj + obase, Cx + obase, alpha);
     }
 }
 
@@ -644,7 +457,7 @@ void k_tile_sp(
     const char* __restrict__ rb = reinterpret_cast<const char*>(brec);
     const uint32_t items = (uint32_t)(nrows * G);
     const bool one = alpha == (T)1;
-    for (uint32_t it = item_block(gridDim.x) * SP_WPB + wv; it < items; it += gridDim.x * SP_WPB) {
+    for (uint32_t it = xcd_block(gridDim.x) * SP_WPB + wv; it < items; it += gridDim.x * SP_WPB) {
         const int g = (int)(it / (uint32_t)nrows);
         const int64_t row = row0 + (int64_t)(it - (uint32_t)g * (uint32_t)nrows);
         const int64_t item = (row - row0) * G + g;
@@ -727,60 +540,7 @@ void k_tile_sp(
                            },
                            [&](int) {});
             wsync();
-#if SPG_SP_WIDE
-            constexpr bool wide = std::is_same<T, double>::value;
-#else
-            constexpr bool wide = false;
-#endif
-            if constexpr (wide) {
-              if ((SPG_TILE_DIAG & 8) == 0) {
-                // 16-byte stores: the values straight from the compact accumulator as pairs, the
-                // columns listed into the freed accumulator (shifted so that 4-aligned output
-                // quads sit at 16-byte LDS offsets) and stored as int32 quads; unaligned heads
-                // and tails entry by entry
-                const int64_t ob = obase + wb;
-                double* __restrict__ xw = reinterpret_cast<double*>(Cx) + ob;
-                const double* acc = reinterpret_cast<const double*>(S.acc);
-                const int vh = (int)(ob & 1);
-                const int np = (wn - vh) >> 1;
-                const double al = (double)alpha;
-                if (l < vh && l < wn) st_c(xw + l, one ? acc[l] : mul_rn(al, acc[l]));
-                for (int i = l; i < np; i += WAVE) {
-                    const int q = vh + 2 * i;
-                    f64x2 x2 = {acc[q], acc[q + 1]};
-                    if (!one) x2 = f64x2{mul_rn(al, x2.x), mul_rn(al, x2.y)};
-                    st_c2(xw + q, x2);
-                }
-                if (l == 0 && np >= 0 && vh + 2 * np < wn) st_c(xw + vh + 2 * np, one ? acc[vh + 2 * np] : mul_rn(al, acc[vh + 2 * np]));
-                wsync();
-                const int ch = (int)((4 - (ob & 3)) & 3), co = 4 - ch;
-                uint32_t* __restrict__ cl = reinterpret_cast<uint32_t*>(S.acc);
-                if (l >= L0 && l < L1) {
-                    int pos = p0 - wb + co;
-#pragma unroll
-                    for (int q = 0; q < SP_WPL; ++q) {
-                        uint32_t w = wd[q];
-                        const int cb = lo + 32 * (w0 + q);
-                        while (w != 0u) {
-                            cl[pos++] = (uint32_t)(cb + __builtin_ctz(w));
-                            w &= w - 1u;
-                        }
-                    }
-                }
-                wsync();
-                int32_t* __restrict__ cw = Cj + ob;
-                const int nq = (wn - ch) >> 2;
-                if (l < ch && l < wn) st_c(cw + l, (int32_t)cl[l + co]);
-                for (int i = l; i < nq; i += WAVE) {
-                    const uint4 c4 = *reinterpret_cast<const uint4*>(&cl[4 * i + 4]);
-                    st_c4(cw + ch + 4 * i, i32x4{(int)c4.x, (int)c4.y, (int)c4.z, (int)c4.w});
-                }
-                {
-                    const int t = ch + 4 * nq + l;
-                    if (nq >= 0 && l < 4 && t < wn && t >= ch) st_c(cw + t, (int32_t)cl[t + co]);
-                }
-              }
-            } else if ((SPG_TILE_DIAG & 8) == 0) {   // (diag 8, timing only: no output)
+            if ((SPG_TILE_DIAG & 8) == 0) {   // (diag 8, timing only: no output)
                 // values: the window's slots are its entries in C order
                 T* __restrict__ xw = Cx + obase + wb;
                 auto vals = [&](auto one) {   // 4 rows of 64 slots per round, reads first
@@ -827,194 +587,6 @@ void k_tile_sp(
             }
             L0 = L1;
         }
-    }
-}
-
-// k-phased sparse tiles (k_tile_sp's walk in PH phases of B rows, as k_tile_dn<.., PH>): the
-// block's waves (as many as the LDS holds: 7 at CAP 2048) meet at a barrier after every phase,
-// so a CU gathers from one 1/PH part of the tile's B slice at a time (config 5's 8192-column
-// slice is 25.8 MB per tile).  Items with several windows walk every window in PH phases; the
-// block runs the most windows any of its items has, idle waves joining the barriers.
-template <typename T, int CAP> constexpr int sp_ph_wpb() {
-    return (int)(158 * 1024 / (sizeof(SpLds<T, CAP>) + 16)) < 8 ? (int)(158 * 1024 / (sizeof(SpLds<T, CAP>) + 16)) : 8;
-}
-template <typename T, typename IP, int SP_CAP, int PH>
-__global__ __launch_bounds__((sp_ph_wpb<T, SP_CAP>() * WAVE)) void k_tile_sp_ph(
-    int64_t row0, int64_t nrows, int tws, int G, const IP* __restrict__ Ap,
-    const int32_t* __restrict__ Aj, const T* __restrict__ Ax, int64_t K,
-    const uint32_t* __restrict__ brec, const int32_t* __restrict__ tptr, const uint32_t* __restrict__ bitmap,
-    const int64_t* __restrict__ item_off, int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha, uint32_t sent) {
-    static_assert(OrderedLdsAdd<T>::value, "ordered LDS add needed");
-    static_assert(sizeof(T) * (SP_CAP + WAVE) >= 4 * SP_CAP, "column list fits the accumulator");
-    constexpr int SP_WPL = SpGeom<SP_CAP>::WPL;
-    constexpr int NB = sizeof(T) > 8 ? 4 : 8;
-    constexpr int WPB = sp_ph_wpb<T, SP_CAP>();
-    __shared__ __attribute__((aligned(16))) SpLds<T, SP_CAP> lds[WPB];
-    __shared__ int nwin_s[WPB];
-    const int l = lane_id();
-    const int wv = uniform((int)(threadIdx.x >> 6));
-    SpLds<T, SP_CAP>& S = lds[wv];
-    const int TW = 1 << tws;
-    const int nw = TW >> 5;
-    const int wpl = (nw + WAVE - 1) / WAVE;
-    const char* __restrict__ rb = reinterpret_cast<const char*>(brec);
-    const uint32_t items = (uint32_t)(nrows * G);
-    const bool one = alpha == (T)1;
-    for (uint32_t base = item_block(gridDim.x) * WPB; base < items; base += gridDim.x * WPB) {
-        const uint32_t it = base + wv;
-        bool live = it < items;
-        int g = 0, nA = 0;
-        int64_t row = 0, item = 0, a0 = 0;
-        if (live) {
-            g = (int)(it / (uint32_t)nrows);
-            row = row0 + (int64_t)(it - (uint32_t)g * (uint32_t)nrows);
-            item = (row - row0) * G + g;
-            a0 = Ap[row];
-            nA = (int)(Ap[row + 1] - a0);
-            live = nA > 0;
-        }
-        const int32_t* __restrict__ tp = tptr + (int64_t)g * (K + 1);
-        const int w0 = min(nw, l * wpl), w1 = min(nw, w0 + wpl);
-        uint32_t wd[SP_WPL] = {};
-        int mine = 0;
-        if (live) {
-            const uint32_t* __restrict__ ibits = bitmap + item * nw;
-#pragma unroll
-            for (int q = 0; q < SP_WPL; ++q)
-                if (w0 + q < w1) {
-                    wd[q] = ibits[w0 + q];
-                    mine += __popc(wd[q]);
-                }
-        }
-        const int pincl = wave_incl_sum_dpp(mine);
-        const int nnz = readlane_i(pincl, WAVE - 1);
-        live = live && nnz > 0;
-        const int p0 = pincl - mine;
-        int32_t kq[NB];
-        T aq[NB];
-        uint2 sq[NB];
-        if (!live) nA = 0;
-#pragma unroll
-        for (int q = 0; q < NB; ++q) {
-            kq[q] = -1;
-            aq[q] = (T)0;
-            if (q * WAVE + l < nA) {
-                kq[q] = ld_a<SP_NT_A>(Aj + a0 + q * WAVE + l);
-                aq[q] = ld_a<SP_NT_A>(Ax + a0 + q * WAVE + l);
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < NB; ++q) sq[q] = kq[q] >= 0 ? seg_pair(tp, kq[q]) : make_uint2(0u, 0u);
-        const int64_t obase = live ? item_off[item] : 0;
-        wsync();
-        if (live) {
-            int run = p0;
-#pragma unroll
-            for (int q = 0; q < SP_WPL; ++q)
-                if (w0 + q < w1) {
-                    S.bw[w0 + q] = make_uint2(wd[q], (uint32_t)run);
-                    run += __popc(wd[q]);
-                }
-        }
-        // the item's windows: lanes [L0, L1) whose words' entries fit SP_CAP slots
-        auto window_end = [&](int L0) {
-            if (nnz <= SP_CAP) return WAVE;
-            const int wb = readlane_i(p0, L0);
-            int L1 = (int)__popcll(__ballot(pincl <= wb + SP_CAP));
-            return L1 <= L0 ? L0 + 1 : L1;
-        };
-        int nwin = 0;
-        if (live)
-            for (int L0 = 0; L0 < WAVE; L0 = window_end(L0)) ++nwin;
-        if (l == 0) nwin_s[wv] = nwin;
-        __syncthreads();
-        int maxwin = 0;
-#pragma unroll
-        for (int q = 0; q < WPB; ++q) maxwin = max(maxwin, nwin_s[q]);
-        const int lo = g * TW;
-        int L0 = 0;
-        for (int w = 0; w < maxwin; ++w) {
-            const bool act = w < nwin;   // (nwin = 0 for dead waves)
-            int L1 = WAVE, wb = 0, wn = nnz;
-            if (act) {
-                L1 = window_end(L0);
-                if (nnz > SP_CAP) {
-                    wb = readlane_i(p0, L0);
-                    wn = (L1 < WAVE ? readlane_i(p0, L1) : nnz) - wb;
-                }
-                wsync();
-                for (int p = l; p < wn; p += WAVE) S.acc[p] = (T)0;
-            }
-            const int clo = 32 * wpl * L0, chi = 32 * wpl * L1;   // window, tile-relative
-            for (int ph = 0; ph < PH; ++ph) {
-                if (act) {
-                    const int klo = (int)(K * ph / PH), khi = (int)(K * (ph + 1) / PH);
-                    int32_t kc[NB];
-                    T ac[NB];
-                    uint2 sc[NB];
-#pragma unroll
-                    for (int q = 0; q < NB; ++q) {
-                        kc[q] = kq[q];
-                        ac[q] = aq[q];
-                        sc[q] = sq[q];
-                    }
-                    dn_walk<T, NB, true>(&S, S.acc, l, tp, a0, nA, ac, sc, Aj, Ax, rb, sent,
-                                         [&](int rc) -> int {
-                                             if (rc < clo || rc >= chi) return SP_CAP + l;   // (sentinels too)
-                                             const uint2 b = S.bw[rc >> 5];
-                                             return (int)b.y + __popc(b.x & ((1u << (rc & 31)) - 1u)) - wb;
-                                         },
-                                         [&](int) {}, &kc, klo, khi);
-                }
-                __syncthreads();
-            }
-            if (act && (SPG_TILE_DIAG & 8) == 0) {
-                wsync();
-                T* __restrict__ xw = Cx + obase + wb;
-                auto vals = [&](auto one) {
-                    for (int q0 = 0; q0 < wn; q0 += 4 * WAVE) {
-                        T v[4];
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) v[e] = S.acc[min(q0 + e * WAVE + l, SP_CAP + WAVE - 1)];
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) {
-                            const int p = q0 + e * WAVE + l;
-                            if (p < wn) st_c(xw + p, decltype(one)::value ? v[e] : mul_rn(alpha, v[e]));
-                        }
-                    }
-                };
-                if (one) vals(std::true_type{});
-                else vals(std::false_type{});
-                wsync();
-                uint32_t* __restrict__ cl = reinterpret_cast<uint32_t*>(S.acc);
-                if (l >= L0 && l < L1) {
-                    int pos = p0 - wb;
-#pragma unroll
-                    for (int q = 0; q < SP_WPL; ++q) {
-                        uint32_t x = wd[q];
-                        const int cb = lo + 32 * (w0 + q);
-                        while (x != 0u) {
-                            cl[pos++] = (uint32_t)(cb + __builtin_ctz(x));
-                            x &= x - 1u;
-                        }
-                    }
-                }
-                wsync();
-                int32_t* __restrict__ cw = Cj + obase + wb;
-                for (int q0 = 0; q0 < wn; q0 += 4 * WAVE) {
-                    uint32_t v[4];
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) v[e] = cl[min(q0 + e * WAVE + l, SP_CAP - 1)];
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const int p = q0 + e * WAVE + l;
-                        if (p < wn) st_c(cw + p, (int32_t)v[e]);
-                    }
-                }
-            }
-            L0 = L1;
-        }
-        __syncthreads();   // (nwin_s is rewritten next round)
     }
 }
 
