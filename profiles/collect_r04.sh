@@ -5,7 +5,7 @@
 set -uo pipefail
 for c in ${WHICH:-4 2 5}; do
   case $c in
-    4) TAG=r04_c4 BENCH_ARGS="--no-config2 --cpu-seconds 0 --steps 3 --warmup 1" PMC_KEY=c4_n65536_d0.005_float64_alg3_w1 \
+    4) TAG=r04_c4 BENCH_ARGS="--no-config2 --no-alg3-chunked --cpu-seconds 0 --steps 3 --warmup 1" PMC_KEY=c4_n65536_d0.005_float64_alg3_w1 \
          PMC_KERNEL="k_tile_dn<double, int" bash profiles/collect.sh || exit 1 ;;
     2) TAG=r04_c2 BENCH_ARGS="--config 2 --cpu-seconds 0" PMC_KEY=c2_n16384_d0.001_float64_alg1_w1 \
          PMC_KERNEL="k_row<double, int, int, 2" bash profiles/collect.sh || exit 1 ;;
