@@ -88,6 +88,10 @@ def parse(argv=None):
                     help="budget of the CPU-baseline sample (0 disables it)")
     ap.add_argument("--no-config2", action="store_true", help="N=1: skip the config2 key")
     ap.add_argument("--no-alg3-chunked", action="store_true", help="N=1: skip the alg3_chunked key")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="N>1: B's values in one broadcast (overlapping the symbolic pass only) instead of "
+                         "tile-major groups overlapping the numeric pass")
+    ap.add_argument("--value-groups", type=int, default=8, help="N>1: column-tile groups of the values broadcast")
     ap.add_argument("--config5-n", type=int, default=262144,
                     help="N>1: size of the strong-scaled config5 key (0 skips it)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
@@ -388,7 +392,9 @@ def run_config4(ctx, args, cfg, tdt, vb, hook):
         bcast_ms = broadcast_ms(ctx, B)
 
         def step():
-            C, _ = distributed.rowblock_step(A, B, 0, ctx.dev, alg=alg, chunk_fraction=cf, multiply=hook)
+            C, _ = distributed.rowblock_step(A, B, 0, ctx.dev, alg=alg, chunk_fraction=cf, multiply=hook,
+                                             pipeline=None if not args.no_pipeline else False,
+                                             n_groups=args.value_groups)
             return C
     else:
         P, nnzB = cusparse.num_products(A, B), B.nnz
@@ -436,6 +442,7 @@ def run_config4(ctx, args, cfg, tdt, vb, hook):
         "peak_hbm_bytes": int(peak_max), "roofline": rf,
         "phases_ms_per_step": {k: round(v[0] / reps, 5) for k, v in ph.items() if v[1]},
         "b_broadcast_ms": None if bcast_ms is None else round(bcast_ms, 3),
+        "b_values_pipeline": None if w == 1 else pipeline_report(ctx, args, A, B, alg, cf, hook, ms),
         "cpu_baseline": cpu,
     }
     del A, B
@@ -456,6 +463,50 @@ def broadcast_ms(ctx, B):
         ts.append(time.perf_counter() - t0)
         del Bt
     return float(np.median(ts)) * 1e3
+
+
+def pipeline_report(ctx, args, A, B, alg, cf, hook, ms):
+    """How much of B's values broadcast the step hides (N > 1): the values broadcast alone
+    (median of 3), the step with the values in one broadcast that overlaps only the
+    symbolic pass (2 steps), and the step as measured.  hidden_ms = unpipelined - measured;
+    overlap_frac = hidden_ms / values_broadcast_ms.  None on the CPU test path."""
+    if not ctx.gpu or hook is not None:
+        return None
+    from spmm_amd import distributed
+    torch = ctx.torch
+    # the values alone (rank 0's B; the others receive into a buffer of its size)
+    meta = torch.tensor([B.nnz, B.data.element_size()] if B is not None else [0, 0], dtype=torch.int64,
+                        device=ctx.dev)
+    ctx.dist.broadcast(meta, 0)
+    nnzB, esz = (int(x) for x in meta.tolist())
+    buf = B.data.view(torch.uint8) if B is not None else torch.empty(nnzB * esz, dtype=torch.uint8, device=ctx.dev)
+    ts = []
+    for _ in range(3):
+        ctx.sync()
+        ctx.barrier()
+        t0 = time.perf_counter()
+        ctx.dist.broadcast(buf, 0)
+        ctx.sync()
+        ctx.barrier()
+        ts.append(time.perf_counter() - t0)
+    vms = float(np.median(ts)) * 1e3
+    pipelined = not args.no_pipeline
+    last = distributed.rowblock_step.last
+
+    def other():
+        C, _ = distributed.rowblock_step(A, B, 0, ctx.dev, alg=alg, chunk_fraction=cf, pipeline=not pipelined,
+                                         n_groups=args.value_groups)
+        return C
+    el, C = timed(ctx, other, 2, 1)
+    del C
+    (el,) = ctx.reduce([el], "max")
+    oms = el / 2 * 1e3
+    ums, pms = (oms, ms) if pipelined else (ms, oms)
+    groups = len(last.groups) if (pipelined and last is not None and last.pipelined) else None
+    return {"pipelined": pipelined and groups is not None, "groups": groups,
+            "values_broadcast_ms": round(vms, 3), "step_ms_unpipelined": round(ums, 4),
+            "step_ms_pipelined": round(pms, 4), "hidden_ms": round(ums - pms, 4),
+            "overlap_frac": round((ums - pms) / vms, 4) if vms > 0 else None}
 
 
 def last_peak(ctx):
@@ -485,7 +536,9 @@ def run_config5(ctx, args, cfg, n, tdt, vb, hook, steps, warmup):
         bcast_ms = broadcast_ms(ctx, B)
 
         def step():
-            C, _ = distributed.rowblock_step(A, B, 0, ctx.dev, alg=alg, chunk_fraction=cf, multiply=hook)
+            C, _ = distributed.rowblock_step(A, B, 0, ctx.dev, alg=alg, chunk_fraction=cf, multiply=hook,
+                                             pipeline=None if not args.no_pipeline else False,
+                                             n_groups=args.value_groups)
             return C
     else:
         A = gen_device(ctx, n, dens, args.seed, tdt)
@@ -512,6 +565,7 @@ def run_config5(ctx, args, cfg, n, tdt, vb, hook, steps, warmup):
            "steps": steps, "warmup": warmup, "scaling": "strong", "N": n, "density": dens, "alg": alg,
            "num_products": int(P_all), "nnzC": int(nnz_all), "rows_rank0": list(rows), "n_chunks": nch,
            "peak_hbm_bytes_max_rank": int(peak_max), "b_broadcast_ms": None if bcast_ms is None else round(bcast_ms, 3),
+           "b_values_pipeline": None if w == 1 else pipeline_report(ctx, args, A, B, alg, cf, hook, ms),
            "roofline_rank0": rf, "phases_ms_per_step": {k: round(v[0] / reps, 5) for k, v in ph.items() if v[1]},
            "workload": (f"{cfg['name']}: random CSR {n}x{n} density={dens:g} {args.dtype}, ALG{alg}; "
                         f"{w} row blocks cut on the product prefix (each rank draws its own block), "

@@ -249,6 +249,28 @@ spg_status_t spg_spgemm_ws(spg_handle_t handle, const spg_csr_t *A, const spg_cs
                            void *C_indptr, spg_index_t C_indptr_type, int64_t *nnzC, void **C_indices,
                            void **C_values, size_t *peak_bytes, spg_plan_t *plan_out);
 
+/* Numeric phase by column-tile groups, for a B whose VALUES arrive in pieces (the multi-GPU
+ * row-block step: B's structure is broadcast first, its values follow group by group and
+ * each group's numeric tiles start as soon as its values land -- the reference broadcasts
+ * a sparse matrix as three grouped payloads, modify_src/cupy-src/cupyx/distributed/
+ * _nccl_comm.py:651-674; no cuSPARSE counterpart: cusparseSpGEMM_compute needs all of B).
+ * Tile-path plans with one row chunk only (spg_plan_info: path 2, n_chunks 1); anything
+ * else returns SPG_STATUS_NOT_SUPPORTED and the caller takes spg_numeric.
+ *   spg_tile_value_offsets: the plan's tiles_per_row + 1 offsets (entries) of each column
+ *     tile's values in TILE-MAJOR order -- B's entries with columns in tile 0 row by row,
+ *     then tile 1, ...  One device->host copy.  The order depends only on B's structure
+ *     and the tile width, so plans on different devices with equal tile widths agree.
+ *   spg_tile_values: B's values (row-major, B->values of the plan) permuted into that
+ *     order (nnz(B) entries of B's value type) -- on the device that holds them.
+ *   spg_numeric_tiles: C's entries in columns of tiles [tile_begin, tile_end) from the
+ *     tile-major values (only that range of them is read), after spg_symbolic, stream-
+ *     ordered like spg_numeric.  Calls over disjoint ranges covering every tile give C
+ *     bit for bit as spg_numeric does; the plan's B->values is never read. */
+spg_status_t spg_tile_value_offsets(spg_handle_t handle, spg_plan_t plan, int64_t *offsets, int64_t capacity);
+spg_status_t spg_tile_values(spg_handle_t handle, spg_plan_t plan, void *tile_major_values);
+spg_status_t spg_numeric_tiles(spg_handle_t handle, spg_plan_t plan, const void *alpha, spg_csr_t *C,
+                               const void *tile_major_values, int64_t tile_begin, int64_t tile_end);
+
 /* Per-phase device timing: with timing enabled every kernel the handle launches is
  * bracketed by hipEvents on the handle's stream, and spg_get_timing returns the
  * accumulated device milliseconds and launch counts per phase (the build's equivalent of

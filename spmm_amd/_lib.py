@@ -38,13 +38,15 @@ STATUS_NAMES = {
 }
 STATUS_ALLOC_FAILED = 2
 STATUS_OVERFLOW = 100
+STATUS_NOT_SUPPORTED = 10
 
 # every symbol include/spgemm.h declares (tests/test_abi.py checks the .so exports them)
 EXPORTS = ("spg_version", "spg_build_info", "spg_status_string", "spg_create", "spg_destroy", "spg_set_stream",
            "spg_last_hip_error", "spg_plan", "spg_num_products", "spg_symbolic",
            "spg_numeric", "spg_peak_bytes", "spg_validate_csr", "spg_plan_destroy",
            "spg_set_timing", "spg_get_timing", "spg_result_in_workspace", "spg_spmv",
-           "spg_spgemm_ws", "spg_plan_info")
+           "spg_spgemm_ws", "spg_plan_info", "spg_tile_value_offsets", "spg_tile_values",
+           "spg_numeric_tiles")
 
 PHASES = ("products", "scan", "symbolic", "numeric", "compact", "validate", "spill", "spmv")
 NUM_PHASES = 8
@@ -119,6 +121,9 @@ def load():
             "spg_spgemm_ws": (ctypes.c_int, [vp, csrp, csrp, ctypes.c_int, ctypes.c_float, vp, vp, sz, vp,
                                              ctypes.c_int, ctypes.POINTER(i64), ctypes.POINTER(vp),
                                              ctypes.POINTER(vp), ctypes.POINTER(sz), ctypes.POINTER(vp)]),
+            "spg_tile_value_offsets": (ctypes.c_int, [vp, vp, ctypes.POINTER(i64), i64]),
+            "spg_tile_values": (ctypes.c_int, [vp, vp, vp]),
+            "spg_numeric_tiles": (ctypes.c_int, [vp, vp, vp, csrp, vp, i64, i64]),
             "spg_set_timing": (ctypes.c_int, [vp, ctypes.c_int]),
             "spg_get_timing": (ctypes.c_int, [vp, ctypes.POINTER(SpgTiming)]),
         }

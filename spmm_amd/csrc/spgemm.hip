@@ -113,7 +113,8 @@ struct spg_plan_s {
     uint32_t* sidx = nullptr;       // symbolic-tile starts inside each B row, B.rows * (Gs + 1)
     void* brec = nullptr;           // tile-major B: (column, value) records (numeric tile pass)
     uint16_t* bj16 = nullptr;       // B's columns modulo 65536 (symbolic tile pass)
-    bool brec_built = false;
+    bool brec_built = false;      // whole records (columns + values) from B
+    bool brec_cols = false;       // their column parts (spg_numeric_tiles fills the values)
     uint32_t* bitmap = nullptr;     // per-item column bitmaps (symbolic -> numeric)
     int64_t* item_cnt = nullptr;    // per-item counts, scanned in place into offsets
     bool tidx_built = false;
@@ -967,20 +968,42 @@ spg_status_t tile_symbolic(spg_handle_t h, spg_plan_s& p, void* cp) {
 
 // spg_numeric on the tile path: the tile-major B records once, then chunk by chunk (the
 // chunk's counts, bitmaps and offsets again when there are several and the tiles are not
-// dense) the numeric tiles.
+// dense) the numeric tiles.  spg_numeric_tiles (tm != nullptr, one chunk): the records'
+// columns once, the values of column tiles [g0, g1) from the tile-major values `tm`, and
+// only those tiles' items.
 template <typename T, typename IP>
-spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T alpha) {
+spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T alpha, int64_t g0 = 0,
+                          int64_t g1 = -1, const T* tm = nullptr) {
+    if (g1 < 0) g1 = p.G;
     const IP* Ap = (const IP*)p.A.indptr;
     const IP* Bp = (const IP*)p.B.indptr;
     const int32_t* Aj = (const int32_t*)p.A.indices;
     const int32_t* Bj = (const int32_t*)p.B.indices;
     const T* Ax = (const T*)p.A.values;
     const T* Bx = (const T*)p.B.values;
-    if (!p.brec_built) {
+    if (tm) {
+        if (!p.brec_cols) {
+            timed_launch(h, SPG_PHASE_SPILL, k_bt_pack<T, IP, 1>, dim3((unsigned)grid_for(p.B.rows, 4)), dim3(256),
+                         p.B.rows, Bp, Bj, Bx, p.tws, (const int32_t*)p.tptr, (uint32_t*)p.brec, p.B.nnz, (T*)nullptr);
+            SPG_LAUNCHED(h);
+            p.brec_cols = true;
+        }
+        p.brec_built = false;   // values of other tiles are stale for a later spg_numeric
+        // records [tptr[g0][0], tptr[g1-1][K]) (the tile-major table is one scan: tile g's
+        // records start where tile g-1's end)
+        const int32_t* tp = (const int32_t*)p.tptr;
+        const int64_t K1 = p.B.rows + 1;
+        const int64_t est = std::max<int64_t>(1, p.B.nnz * (g1 - g0) / std::max<int64_t>(p.G, 1));
+        timed_launch(h, SPG_PHASE_SPILL, k_bt_fill<T>,
+                     dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(grid_for(est, 256), 16384))), dim3(256),
+                     tp + g0 * K1, tp + (g1 - 1) * K1 + p.B.rows, tm, (uint32_t*)p.brec);
+        SPG_LAUNCHED(h);
+    } else if (!p.brec_built) {
         timed_launch(h, SPG_PHASE_SPILL, k_bt_pack<T, IP>, dim3((unsigned)grid_for(p.B.rows, 4)), dim3(256), p.B.rows,
-                     Bp, Bj, Bx, p.tws, (const int32_t*)p.tptr, (uint32_t*)p.brec, p.B.nnz);
+                     Bp, Bj, Bx, p.tws, (const int32_t*)p.tptr, (uint32_t*)p.brec, p.B.nnz, (T*)nullptr);
         SPG_LAUNCHED(h);
         p.brec_built = true;
+        p.brec_cols = true;
     }
     // byte offset of sentinel region r after B's records (k_bt_pack)
     auto sent = [&](int r) {
@@ -992,6 +1015,9 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
         if (nch > 1 && !tile_dense(p) && (st = tile_sym_chunk<IP>(h, p, c))) return st;
         const int64_t r0 = tile_chunk_r0(p, c), n = tile_chunk_r1(p, c) - r0;
         if (n <= 0) continue;
+        // the items of tiles [g0, g1) (host keeps rows*G < 2^31)
+        const uint32_t it_lo = (uint32_t)(g0 * n), it_hi = (uint32_t)(g1 * n);
+        const int64_t nit = (g1 - g0) * n;
         KernelTimer kt(h, SPG_PHASE_NUMERIC);
         // dense accumulator when the tile fits one window; round groups (tile_variant())
         const bool dense = tile_dense(p);
@@ -1000,21 +1026,21 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
             constexpr bool DN = decltype(dn)::value;
             constexpr int RN = decltype(rn)::value;
             constexpr int WPBN = tile_num_wpb<DN>();
-            hipExtLaunchKernelGGL((k_tile<T, IP, DN, RN>), dim3(tile_grid(n * p.G, WPBN)), dim3(WPBN * WAVE), 0,
+            hipExtLaunchKernelGGL((k_tile<T, IP, DN, RN>), dim3(tile_grid(nit, WPBN)), dim3(WPBN * WAVE), 0,
                                   h->stream, kt.a, kt.b, 0, r0, n, p.tws, p.G, Ap, Aj, Ax, p.B.rows,
                                   (const uint32_t*)p.brec, (const int32_t*)p.tptr,
                                   dense ? (const uint32_t*)nullptr : (const uint32_t*)p.bitmap,
-                                  (const int64_t*)tile_chunk_items(p, c), cj, cx, alpha);
+                                  (const int64_t*)tile_chunk_items(p, c), cj, cx, alpha, it_lo, it_hi);
         };
         if constexpr (OrderedLdsAdd<T>::value) {
             if (!dense && p.lean && SPG_SP_LEAN) {   // sparse tiles, ordered LDS adds
                 auto sp = [&](auto capc) {
                     constexpr int CAP = decltype(capc)::value;
-                    hipExtLaunchKernelGGL((k_tile_sp<T, IP, CAP>), dim3(tile_grid(n * p.G, SP_WPB)), dim3(SP_WPB * WAVE),
+                    hipExtLaunchKernelGGL((k_tile_sp<T, IP, CAP>), dim3(tile_grid(nit, SP_WPB)), dim3(SP_WPB * WAVE),
                                           0, h->stream, kt.a, kt.b, 0, r0, n, p.tws, p.G, Ap, Aj, Ax, p.B.rows,
                                           (const uint32_t*)p.brec, (const int32_t*)p.tptr, (const uint32_t*)p.bitmap,
                                           (const int64_t*)tile_chunk_items(p, c), cj, cx, alpha,
-                                          sent(2));   // (sparse tiles' region)
+                                          sent(2), it_lo, it_hi);   // (sparse tiles' region)
                 };
                 if constexpr (std::is_same<T, double>::value) {
                     if (p.tws > 12) sp(std::integral_constant<int, 2048>{});
@@ -1028,11 +1054,11 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
             if (dense && p.lean) {   // ordered LDS adds (spgemm_tile_dn.hpp)
                 auto dn = [&](auto twd) {
                     constexpr int TWD = decltype(twd)::value;
-                    hipExtLaunchKernelGGL((k_tile_dn<T, IP, TWD>), dim3(tile_grid(n * p.G, DN_WPB)), dim3(DN_WPB * WAVE),
+                    hipExtLaunchKernelGGL((k_tile_dn<T, IP, TWD>), dim3(tile_grid(nit, DN_WPB)), dim3(DN_WPB * WAVE),
                                           0, h->stream, kt.a, kt.b, 0, r0, n, p.tws, p.G, Ap, Aj, Ax, p.B.rows,
                                           (const uint32_t*)p.brec, (const int32_t*)p.tptr,
                                           (const int64_t*)tile_chunk_items(p, c), cj, cx, alpha,
-                                          sent(sentinel_region(TWD)));
+                                          sent(sentinel_region(TWD)), it_lo, it_hi);
                 };
                 if constexpr (std::is_same<T, double>::value) {
                     if ((1 << p.tws) > 1024) dn(std::integral_constant<int, 2048>{});
@@ -1662,6 +1688,84 @@ spg_status_t spg_numeric(spg_handle_t h, spg_plan_t p, const void* alpha, spg_cs
                             : numeric_typed<T, int64_t, int32_t>(h, *p, *C, a);
         return c64 ? numeric_typed<T, int32_t, int64_t>(h, *p, *C, a)
                    : numeric_typed<T, int32_t, int32_t>(h, *p, *C, a);
+    });
+}
+
+// ---- the numeric phase by column-tile groups (include/spgemm.h; multi-GPU B-value pipelining)
+static spg_status_t tiles_supported(spg_plan_t p) {
+    if (!p) return SPG_STATUS_INVALID_VALUE;
+    if (!p->use_tile || tile_chunks(*p) != 1 || p->alg1_fused) return SPG_STATUS_NOT_SUPPORTED;
+    if (!p->tidx_built) return SPG_STATUS_NOT_INITIALIZED;   // spg_symbolic builds the table
+    return SPG_STATUS_SUCCESS;
+}
+
+spg_status_t spg_tile_value_offsets(spg_handle_t h, spg_plan_t p, int64_t* offsets, int64_t capacity) {
+    if (!h) return SPG_STATUS_NOT_INITIALIZED;
+    spg_status_t st = tiles_supported(p);
+    if (st) return st;
+    if (capacity < p->G + 1 || !offsets) return SPG_STATUS_INVALID_VALUE;
+    DeviceGuard dg_(h->device);
+    SPG_HIP(h, dg_.err);
+    // tile g starts at table word g*(K+1); the last tile's end slot holds nnz(B)
+    const int64_t K1 = p->B.rows + 1;
+    std::vector<int32_t> w((size_t)p->G + 1);
+    SPG_HIP(h, hipMemcpy2DAsync(w.data(), sizeof(int32_t), p->tptr, (size_t)K1 * sizeof(int32_t), sizeof(int32_t),
+                                (size_t)p->G, hipMemcpyDeviceToHost, h->stream));
+    SPG_HIP(h, hipMemcpyAsync(w.data() + p->G, (const int32_t*)p->tptr + (p->G - 1) * K1 + p->B.rows,
+                              sizeof(int32_t), hipMemcpyDeviceToHost, h->stream));
+    SPG_HIP(h, hipStreamSynchronize(h->stream));
+    for (int64_t g = 0; g <= p->G; ++g) offsets[g] = w[(size_t)g];
+    return SPG_STATUS_SUCCESS;
+}
+
+spg_status_t spg_tile_values(spg_handle_t h, spg_plan_t p, void* tm) {
+    if (!h) return SPG_STATUS_NOT_INITIALIZED;
+    spg_status_t st = tiles_supported(p);
+    if (st) return st;
+    if (!tm && p->B.nnz > 0) return SPG_STATUS_INVALID_VALUE;
+    if (p->B.nnz > 0 && !p->B.values) return SPG_STATUS_INVALID_VALUE;
+    if (p->B.rows == 0 || p->B.nnz == 0) return SPG_STATUS_SUCCESS;
+    DeviceGuard dg_(h->device);
+    SPG_HIP(h, dg_.err);
+    const bool i64 = p->A.indptr_type == SPG_INDEX_64I;
+    return dispatch_value(p->A.value_type, [&](auto tag) {
+        using T = decltype(tag);
+        auto go = [&](auto ip) {
+            using IP = decltype(ip);
+            timed_launch(h, SPG_PHASE_SPILL, k_bt_pack<T, IP, 2>, dim3((unsigned)grid_for(p->B.rows, 4)), dim3(256),
+                         p->B.rows, (const IP*)p->B.indptr, (const int32_t*)p->B.indices, (const T*)p->B.values,
+                         p->tws, (const int32_t*)p->tptr, (uint32_t*)p->brec, p->B.nnz, (T*)tm);
+        };
+        if (i64) go(int64_t{}); else go(int32_t{});
+        SPG_LAUNCHED(h);
+        return SPG_STATUS_SUCCESS;
+    });
+}
+
+spg_status_t spg_numeric_tiles(spg_handle_t h, spg_plan_t p, const void* alpha, spg_csr_t* C, const void* tm,
+                               int64_t g0, int64_t g1) {
+    if (!h) return SPG_STATUS_NOT_INITIALIZED;
+    if (!p || !alpha || !C) return SPG_STATUS_INVALID_VALUE;
+    if (p->nnzC < 0) return SPG_STATUS_NOT_INITIALIZED;     // spg_symbolic first
+    spg_status_t st = tiles_supported(p);
+    if (st) return st;
+    if (g0 < 0 || g1 > p->G || g0 > g1) return SPG_STATUS_INVALID_VALUE;
+    if (C->rows != p->A.rows || C->cols != p->B.cols) return SPG_STATUS_INVALID_VALUE;
+    if (C->value_type != p->A.value_type) return SPG_STATUS_INVALID_VALUE;
+    if (C->indptr != p->c_indptr || C->indptr_type != p->c_indptr_type) return SPG_STATUS_INVALID_VALUE;
+    if (C->nnz != p->nnzC) return SPG_STATUS_INVALID_VALUE;
+    if (p->nnzC > 0 && (!C->indices || !C->values)) return SPG_STATUS_INVALID_VALUE;
+    if (p->B.nnz > 0 && !tm) return SPG_STATUS_INVALID_VALUE;
+    if (p->nnzC == 0 || g0 == g1) return SPG_STATUS_SUCCESS;
+    DeviceGuard dg_(h->device);
+    SPG_HIP(h, dg_.err);
+    const bool i64 = p->A.indptr_type == SPG_INDEX_64I;
+    return dispatch_value(p->A.value_type, [&](auto tag) {
+        using T = decltype(tag);
+        T a;
+        std::memcpy(&a, alpha, sizeof(T));
+        return i64 ? tile_numeric<T, int64_t>(h, *p, (int32_t*)C->indices, (T*)C->values, a, g0, g1, (const T*)tm)
+                   : tile_numeric<T, int32_t>(h, *p, (int32_t*)C->indices, (T*)C->values, a, g0, g1, (const T*)tm);
     });
 }
 

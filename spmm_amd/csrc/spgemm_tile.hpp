@@ -172,6 +172,29 @@ __device__ __forceinline__ void store_rec(uint32_t* __restrict__ rec, int64_t i,
     q[W - 1] = (uint32_t)lc;
 }
 
+// The column part / the value part of a record alone (spg_numeric_tiles: columns from B's
+// structure first, values group by group as they arrive).
+template <typename T>
+__device__ __forceinline__ void store_rec_col(uint32_t* __restrict__ rec, int64_t i, int lc) {
+    if constexpr (rec_bytes<T>() == 10) {
+        reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(rec) + i * 10)[4] = (uint16_t)lc;
+    } else {
+        rec[i * rec_words<T>() + rec_words<T>() - 1] = (uint32_t)lc;
+    }
+}
+template <typename T>
+__device__ __forceinline__ void store_rec_val(uint32_t* __restrict__ rec, int64_t i, T v) {
+    if constexpr (rec_bytes<T>() == 10) {
+        uint16_t* q = reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(rec) + i * 10);
+        uint64_t b;
+        __builtin_memcpy(&b, &v, 8);
+#pragma unroll
+        for (int h = 0; h < 4; ++h) q[h] = (uint16_t)(b >> (16 * h));
+    } else {
+        __builtin_memcpy(rec + i * rec_words<T>(), &v, sizeof(T));
+    }
+}
+
 // Sentinel records after B's nnz records: the lean tile kernels point every product slot past
 // the end of a batch at them instead of masking the slot (no compare / select per chunk).
 // Regions 0 and 1 (dense tiles of 1024 / 2048 columns): columns 1024 / 2048 + (i % 32),
@@ -220,14 +243,17 @@ __global__ __launch_bounds__(256) void k_bt_count(int64_t K, int G, int R, const
 // segment's first entry, found by a max-scan over the lanes where the tile id steps.
 // (The grid's first SENT_REGIONS * SENT_N threads also write the sentinel records after the
 // nnz(B) real ones.)
-template <typename T, typename IP>
+// MODE 0: whole records; 1: the column parts and the sentinels only (values come later,
+// k_bt_fill); 2: the values alone, densely in record order into `tm` (spg_tile_values).
+template <typename T, typename IP, int MODE = 0>
 __global__ __launch_bounds__(256) void k_bt_pack(int64_t K, const IP* __restrict__ Bp, const int32_t* __restrict__ Bj,
                                                  const T* __restrict__ Bx, int tws,
                                                  const int32_t* __restrict__ tptr, uint32_t* __restrict__ rec,
-                                                 int64_t nnzB) {
+                                                 int64_t nnzB, T* __restrict__ tm = nullptr) {
     const int l = lane_id();
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < SENT_REGIONS * SENT_N; i += gridDim.x * 256)
-        store_rec(rec, nnzB + i, sentinel_col(i), (T)0);
+    if (MODE != 2)
+        for (int i = blockIdx.x * 256 + threadIdx.x; i < SENT_REGIONS * SENT_N; i += gridDim.x * 256)
+            store_rec(rec, nnzB + i, sentinel_col(i), (T)0);
     const int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (k >= K) return;
     const IP r0 = Bp[k];
@@ -242,8 +268,23 @@ __global__ __launch_bounds__(256) void k_bt_pack(int64_t K, const IP* __restrict
         if (l == 0) gp = e0 == 0 ? -1 : (Bj[r0 + e0 - 1] >> tws);
         const int s0 = max(wave_incl_max_dpp((in && g != gp) ? e : -1), carry);
         carry = readlane_i(s0, WAVE - 1);
-        if (in) store_rec(rec, (int64_t)tptr[(int64_t)g * (K + 1) + k] + (e - s0), c & ((1 << tws) - 1), Bx[r0 + e]);
+        if (in) {
+            const int64_t at = (int64_t)tptr[(int64_t)g * (K + 1) + k] + (e - s0);
+            if constexpr (MODE == 0) store_rec(rec, at, c & ((1 << tws) - 1), Bx[r0 + e]);
+            else if constexpr (MODE == 1) store_rec_col<T>(rec, at, c & ((1 << tws) - 1));
+            else tm[at] = Bx[r0 + e];
+        }
     }
+}
+
+// Value parts of records [*lo, *hi) from the tile-major values (the bounds are segment-table
+// words, read on the device: the host never waits for them).
+template <typename T>
+__global__ __launch_bounds__(256) void k_bt_fill(const int32_t* __restrict__ lo, const int32_t* __restrict__ hi,
+                                                 const T* __restrict__ tm, uint32_t* __restrict__ rec) {
+    const int64_t r0 = *lo, r1 = *hi;
+    for (int64_t r = r0 + (int64_t)blockIdx.x * 256 + threadIdx.x; r < r1; r += (int64_t)gridDim.x * 256)
+        store_rec_val<T>(rec, r, tm[r]);
 }
 
 // (start, end) of B row k's segment in a tile: two adjacent table words with one 8-byte
@@ -580,7 +621,7 @@ __global__ __launch_bounds__(tile_num_wpb<DENSE>() * WAVE) void k_tile(
     const int32_t* __restrict__ Aj, const T* __restrict__ Ax, int64_t K,
     const uint32_t* __restrict__ brec, const int32_t* __restrict__ tptr,
     const uint32_t* __restrict__ bitmap, const int64_t* __restrict__ item_off,
-    int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha) {
+    int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha, uint32_t it_lo, uint32_t it_hi) {
     constexpr int diag = SPG_TILE_DIAG;   // 0 in every shipped build (timing-only diagnostics)
     constexpr int U = sizeof(T) > 8 ? 4 : 8;   // chunks in flight (complex128: half)
     static_assert(U % RU == 0, "round groups split the chunks in flight");
@@ -592,8 +633,8 @@ __global__ __launch_bounds__(tile_num_wpb<DENSE>() * WAVE) void k_tile(
     const int TW = 1 << tws;
     const int nw = TW >> 5;                    // bitmap words of a tile
     const int wpl = (nw + WAVE - 1) / WAVE;    // words per lane (<= 2)
-    const uint32_t items = (uint32_t)(nrows * G);   // host keeps rows*G < 2^31
-    for (uint32_t it = xcd_block(gridDim.x) * WPB + wv; it < items; it += gridDim.x * WPB) {
+    // items [it_lo, it_hi) (tile-major: a range of whole tiles; rows*G < 2^31 on the host)
+    for (uint32_t it = it_lo + xcd_block(gridDim.x) * WPB + wv; it < it_hi; it += gridDim.x * WPB) {
         const int g = (int)(it / (uint32_t)nrows);
         const int64_t row = row0 + (int64_t)(it - (uint32_t)g * (uint32_t)nrows);
         const int64_t item = (row - row0) * G + g;   // items (and bitmaps) of this chunk of rows

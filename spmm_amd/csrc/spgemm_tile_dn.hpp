@@ -371,7 +371,8 @@ __global__ __launch_bounds__(DN_WPB * WAVE) void k_tile_dn(
     int64_t row0, int64_t nrows, int tws, int G, const IP* __restrict__ Ap,
     const int32_t* __restrict__ Aj, const T* __restrict__ Ax, int64_t K,
     const uint32_t* __restrict__ brec, const int32_t* __restrict__ tptr,
-    const int64_t* __restrict__ item_off, int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha, uint32_t sent) {
+    const int64_t* __restrict__ item_off, int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha, uint32_t sent,
+    uint32_t it_lo, uint32_t it_hi) {
     static_assert(OrderedLdsAdd<T>::value, "ordered LDS add needed");
     constexpr int NB = sizeof(T) > 8 ? 4 : 8;    // A batches preloaded per item
     __shared__ __attribute__((aligned(16))) DnLds<T, TWD> lds[DN_WPB];
@@ -380,8 +381,8 @@ __global__ __launch_bounds__(DN_WPB * WAVE) void k_tile_dn(
     DnLds<T, TWD>& S = lds[wv];
     const int TW = 1 << tws;
     const char* __restrict__ rb = reinterpret_cast<const char*>(brec);
-    const uint32_t items = (uint32_t)(nrows * G);   // host keeps rows*G < 2^31
-    for (uint32_t it = xcd_block(gridDim.x) * DN_WPB + wv; it < items; it += gridDim.x * DN_WPB) {
+    // items [it_lo, it_hi) (tile-major: a range of whole tiles; rows*G < 2^31 on the host)
+    for (uint32_t it = it_lo + xcd_block(gridDim.x) * DN_WPB + wv; it < it_hi; it += gridDim.x * DN_WPB) {
         const int g = (int)(it / (uint32_t)nrows);
         const int64_t row = row0 + (int64_t)(it - (uint32_t)g * (uint32_t)nrows);
         const int64_t item = (row - row0) * G + g;
@@ -442,7 +443,8 @@ void k_tile_sp(
     int64_t row0, int64_t nrows, int tws, int G, const IP* __restrict__ Ap,
     const int32_t* __restrict__ Aj, const T* __restrict__ Ax, int64_t K,
     const uint32_t* __restrict__ brec, const int32_t* __restrict__ tptr, const uint32_t* __restrict__ bitmap,
-    const int64_t* __restrict__ item_off, int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha, uint32_t sent) {
+    const int64_t* __restrict__ item_off, int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha, uint32_t sent,
+    uint32_t it_lo, uint32_t it_hi) {
     static_assert(OrderedLdsAdd<T>::value, "ordered LDS add needed");
     static_assert(sizeof(T) * (SP_CAP + WAVE) >= 4 * SP_CAP, "column list fits the accumulator");
     constexpr int SP_WPL = SpGeom<SP_CAP>::WPL;
@@ -455,9 +457,8 @@ void k_tile_sp(
     const int nw = TW >> 5;                    // bitmap words of a tile
     const int wpl = (nw + WAVE - 1) / WAVE;    // words per lane (<= SP_WPL)
     const char* __restrict__ rb = reinterpret_cast<const char*>(brec);
-    const uint32_t items = (uint32_t)(nrows * G);
     const bool one = alpha == (T)1;
-    for (uint32_t it = xcd_block(gridDim.x) * SP_WPB + wv; it < items; it += gridDim.x * SP_WPB) {
+    for (uint32_t it = it_lo + xcd_block(gridDim.x) * SP_WPB + wv; it < it_hi; it += gridDim.x * SP_WPB) {
         const int g = (int)(it / (uint32_t)nrows);
         const int64_t row = row0 + (int64_t)(it - (uint32_t)g * (uint32_t)nrows);
         const int64_t item = (row - row0) * G + g;

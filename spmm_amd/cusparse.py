@@ -118,12 +118,21 @@ def spgemm(a, b, alpha=1, alg=0, chunk_fraction=0.2, verbose=False):
     return _spgemm(a, b, alpha, alg, chunk_fraction, verbose)
 
 
-def _spgemm(a, b, alpha=1, alg=0, chunk_fraction=0.2, verbose=False, before_numeric=None):
+def _spgemm(a, b, alpha=1, alg=0, chunk_fraction=0.2, verbose=False, before_numeric=None, by_tiles=None):
     """spgemm, plus `before_numeric`: a callable run after the symbolic pass and before the
     numeric pass reads the values (the multi-GPU path waits there for B's values to arrive
     over RCCL; spmm_amd.distributed).  With it the call takes the ctypes path (the native
     shim runs both passes in one call); ALG1 runs it first (its count and numeric passes
-    are queued together)."""
+    are queued together).
+
+    `by_tiles(geom)`: the numeric pass by column-tile groups (spg_numeric_tiles), called
+    exactly once per product, after the symbolic pass.  `geom` is None when the plan cannot
+    run by tiles (not the tile path, several row chunks, ALG1); then `by_tiles` makes
+    b.data complete and returns None, and spg_numeric runs.  Otherwise geom is a dict
+    (tile_width, tiles, offsets: the tiles + 1 tile-major value offsets, tile_values(): B's
+    values permuted tile-major by this plan) and `by_tiles` returns (tm, groups): the
+    tile-major values tensor and an iterable of (tile_begin, tile_end) ranges, each yielded
+    once its slice of tm is ready on the current stream, together covering every tile."""
     if not check_availability("spgemm"):
         raise RuntimeError("spgemm is not available.")
     assert a.ndim == b.ndim == 2
@@ -152,10 +161,14 @@ def _spgemm(a, b, alpha=1, alg=0, chunk_fraction=0.2, verbose=False, before_nume
     dev = a.device
     h = _handle_for(a)
     cf = float(chunk_fraction)
-    fp = _fastpath.get() if before_numeric is None else None
+    fp = _fastpath.get() if before_numeric is None and by_tiles is None else None
     if before_numeric is not None and algo == _lib.SPG_ALG1:
         before_numeric()
         before_numeric = None
+    if by_tiles is not None and algo == _lib.SPG_ALG1:
+        if by_tiles(None) is not None:
+            raise RuntimeError("by_tiles must complete B's values when geom is None")
+        by_tiles = None
     if fp is not None:   # the same sequence in one native call (csrc/fastpath.cpp)
         al = complex(alpha)
         st, data, indices, indptr, wsb, peak = fp.spgemm(
@@ -209,7 +222,10 @@ def _spgemm(a, b, alpha=1, alg=0, chunk_fraction=0.2, verbose=False, before_nume
                         data.data_ptr() if nnzc else 0, _IT[indptr.dtype], _VT[data.dtype])
             if before_numeric is not None:
                 before_numeric()
-            check(lib.spg_numeric(h.ptr, plan, ctypes.byref(al), ctypes.byref(vc)), "spg_numeric")
+            if by_tiles is not None and _numeric_by_tiles(h, plan, b, al, vc, by_tiles):
+                pass
+            else:
+                check(lib.spg_numeric(h.ptr, plan, ctypes.byref(al), ctypes.byref(vc)), "spg_numeric")
         finally:
             lib.spg_plan_destroy(plan)
     if wide and nnzc < 2 ** 31:
@@ -217,6 +233,45 @@ def _spgemm(a, b, alpha=1, alg=0, chunk_fraction=0.2, verbose=False, before_nume
     last_stats.alg, last_stats.workspace_bytes = int(algo), int(ws_bytes.value)
     last_stats.peak_bytes, last_stats.nnz = int(peak.value), nnzc
     return csr_matrix._from_parts(data, indices, indptr, (m, n), canonical=True)
+
+
+def _numeric_by_tiles(h, plan, b, al, vc, by_tiles) -> bool:
+    """The numeric pass through spg_numeric_tiles, group by group as `by_tiles` releases
+    them (see _spgemm).  False when `by_tiles` took the spg_numeric fallback."""
+    lib = h.lib
+    info = _lib.SpgPlanInfo()
+    check(lib.spg_plan_info(plan, ctypes.byref(info), None, 0), "spg_plan_info")
+    geom = None
+    if info.path == 2 and info.n_chunks == 1:
+        G = int(info.tiles_per_row)
+        offs = (ctypes.c_int64 * (G + 1))()
+        st = lib.spg_tile_value_offsets(h.ptr, plan, offs, G + 1)
+        if st == 0:
+            def tile_values():
+                tm = torch.empty(max(b.nnz, 1), dtype=b.data.dtype, device=b.data.device)
+                check(lib.spg_tile_values(h.ptr, plan, ctypes.c_void_p(tm.data_ptr())), "spg_tile_values")
+                return tm[:b.nnz]
+            geom = {"tile_width": int(info.tile_width), "tiles": G, "offsets": np.frombuffer(offs, dtype=np.int64).copy(),
+                    "tile_values": tile_values}
+        elif st != _lib.STATUS_NOT_SUPPORTED:
+            check(st, "spg_tile_value_offsets")
+    got = by_tiles(geom)
+    if got is None:
+        return False
+    if geom is None:
+        raise RuntimeError("by_tiles returned tile groups for a plan that cannot run by tiles")
+    tm, groups = got
+    covered = 0
+    for g0, g1 in groups:
+        if g0 != covered:
+            raise RuntimeError(f"tile groups must be consecutive: expected {covered}, got {g0}")
+        check(lib.spg_numeric_tiles(h.ptr, plan, ctypes.byref(al), ctypes.byref(vc),
+                                    ctypes.c_void_p(tm.data_ptr() if tm.numel() else 0), int(g0), int(g1)),
+              "spg_numeric_tiles")
+        covered = g1
+    if covered != geom["tiles"]:
+        raise RuntimeError(f"tile groups covered {covered} of {geom['tiles']} tiles")
+    return True
 
 
 def spmv(a, x, y=None, alpha=1, beta=0, transa=False):

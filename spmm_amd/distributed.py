@@ -13,6 +13,14 @@ cross-GPU reduction.  The collectives are
   torch.distributed.  With ``async_values=True`` the values broadcast is left in flight and
   its work handle returned, so the symbolic pass (which reads only B's structure) runs
   while the values arrive (``spgemm_rowblock``'s ``before_numeric`` waits for them);
+* ``broadcast_tile_values`` (``rowblock_step(..., pipeline=True)``, the default on GPUs):
+  B's structure as above, then the symbolic pass, then B's values in TILE-MAJOR order
+  (spg_tile_values on ``src``: the entries of column tile 0 row by row, then tile 1, ...)
+  as one async broadcast per group of column tiles; each group's numeric tiles
+  (spg_numeric_tiles) start when its slice lands, so the values broadcast overlaps the
+  numeric pass, not only the symbolic pass.  The ranks first agree (one 3-int64
+  all_gather) that every plan runs by tiles with the same tile width; otherwise the step
+  falls back to the row-major values broadcast and spg_numeric;
 * ``allgather_nnz``: every rank's nnz(C slab) -> global row-pointer offsets, when a
   stitched C is wanted.
 
@@ -38,12 +46,15 @@ def _bytes_of(t: torch.Tensor) -> torch.Tensor:
     return t.contiguous().view(-1).view(torch.uint8)
 
 
-def broadcast_csr(M: csr_matrix | None, src: int, device, group=None, async_values: bool = False):
+def broadcast_csr(M: csr_matrix | None, src: int, device, group=None, async_values: bool = False,
+                  values: bool = True):
     """Broadcast a CSR matrix held by rank `src` to every rank of `group`.
 
     Returns the matrix, or ``(matrix, work)`` with ``async_values=True``: the values
     broadcast is still in flight and ``work.wait()`` orders the current stream after it
-    (``work`` is None when there is nothing to wait for)."""
+    (``work`` is None when there is nothing to wait for).  ``values=False`` broadcasts the
+    structure only: off `src` the matrix's values are an uninitialised buffer (filled later,
+    e.g. by ``send_values``)."""
     rank = dist.get_rank(group)
     meta = torch.zeros(6, dtype=torch.int64, device=device)
     if rank == src:
@@ -63,7 +74,7 @@ def broadcast_csr(M: csr_matrix | None, src: int, device, group=None, async_valu
         data = torch.empty(nnz, dtype=_CODE_DT[dtc], device=device)
     dist.broadcast(struct, src, group=group)
     work = None
-    if nnz:
+    if nnz and values:
         if async_values:
             work = dist.broadcast(_bytes_of(data), src, group=group, async_op=True)
         else:
@@ -162,17 +173,112 @@ def rowblock_setup_drawn(draw, n_rows: int, b_indptr: torch.Tensor, world: int, 
     return (r0, r1), A, int(pref[r1] - pref[r0])
 
 
+def tile_groups(offsets, n_groups: int):
+    """Consecutive column-tile ranges [(g0, g1)] for the pipelined values broadcast: about
+    equal VALUE counts per group (cut on the tile-major offsets), at most n_groups, every
+    group non-empty in tiles."""
+    offs = np.asarray(offsets, dtype=np.int64)
+    G = len(offs) - 1
+    k = max(1, min(int(n_groups), G))
+    cuts = [0]
+    for i in range(1, k):
+        c = int(np.searchsorted(offs, (int(offs[-1]) * i) // k, side="left"))
+        cuts.append(min(max(c, cuts[-1] + 1), G - (k - i)))
+    cuts.append(G)
+    return [(cuts[i], cuts[i + 1]) for i in range(k)]
+
+
+def agree_tiles(geom, device, group=None) -> bool:
+    """Every rank's plan runs by tiles with the same tile width and count (one 3-int64
+    all_gather; a collective every rank calls once per step)."""
+    world = dist.get_world_size(group)
+    if dist.get_backend(group) != "nccl":
+        device = "cpu"   # gloo (the rehearsal on one GPU) gathers host tensors
+    mine = torch.tensor([1, geom["tile_width"], geom["tiles"]] if geom is not None else [0, 0, 0],
+                        dtype=torch.int64, device=device)
+    out = [torch.zeros(3, dtype=torch.int64, device=device) for _ in range(world)]
+    dist.all_gather(out, mine, group=group)
+    rows = [tuple(int(v) for v in t.tolist()) for t in out]
+    return rows[0][0] == 1 and all(r == rows[0] for r in rows)
+
+
+class TileValueBroadcast:
+    """The `by_tiles` protocol of cusparse._spgemm for one row-block step (see module doc):
+    agree on the tile geometry, then `src` permutes B's values tile-major and every group
+    goes out as its own async broadcast; receivers yield a group once its work is waited
+    on (the current stream is ordered after it).  On disagreement the row-major values go
+    out in one broadcast and spg_numeric runs.  After the product, `overlap` holds
+    (groups, values bytes) for the report; `finish()` orders the current stream after
+    every broadcast (the source's numeric tiles do not wait for its own sends)."""
+
+    def __init__(self, B: csr_matrix, src: int, device, group=None, n_groups: int = 8):
+        self.B, self.src, self.device, self.group, self.n_groups = B, src, device, group, n_groups
+        self.works = []
+        self.pipelined = False
+        self.groups = []
+
+    def __call__(self, geom):
+        rank = dist.get_rank(self.group)
+        if not agree_tiles(geom, self.device, self.group):
+            if self.B.nnz:
+                dist.broadcast(_bytes_of(self.B.data), self.src, group=self.group)
+            return None
+        self.pipelined = True
+        offs = geom["offsets"]
+        if rank == self.src:
+            tm = geom["tile_values"]()
+        else:
+            tm = torch.empty(self.B.nnz, dtype=self.B.data.dtype, device=self.device)
+        self.groups = tile_groups(offs, self.n_groups)
+        works = []
+        for g0, g1 in self.groups:
+            a, b = int(offs[g0]), int(offs[g1])
+            works.append(dist.broadcast(_bytes_of(tm[a:b]), self.src, group=self.group, async_op=True)
+                         if b > a else None)
+        self.works = works
+        return tm, self._release(rank)
+
+    def _release(self, rank):
+        for (g0, g1), w in zip(self.groups, self.works):
+            if w is not None and rank != self.src:
+                w.wait()
+            yield g0, g1
+
+    def finish(self):
+        for w in self.works:
+            if w is not None:
+                w.wait()
+        self.works = []
+
+
 def rowblock_step(A_block: csr_matrix, B_src: csr_matrix | None, src: int, device, alg: int = 2,
-                  chunk_fraction: float = 0.2, multiply=None, group=None):
+                  chunk_fraction: float = 0.2, multiply=None, group=None, pipeline: bool | None = None,
+                  n_groups: int = 8):
     """One C = A.B step of the row-block scheme on this rank: B arrives from `src` (its
     structure first; the values stay in flight through the symbolic pass), then this
     rank's slab A_block . B.  `multiply(A_block, B, wait_values)` replaces the device
-    multiply (the gloo tests run the CPU oracle there).  Returns (C slab, B)."""
+    multiply (the gloo tests run the CPU oracle there).  `pipeline` (default: on a GPU
+    device): the values travel tile-major in `n_groups` async broadcasts, each group's
+    numeric tiles starting as its slice lands (TileValueBroadcast).  Returns (C slab, B);
+    after a pipelined step B's values are row-major on `src` only."""
+    if pipeline is None:
+        pipeline = multiply is None and torch.device(device).type == "cuda"
+    if pipeline and multiply is None:
+        B, _ = broadcast_csr(B_src, src, device, group, async_values=True, values=False)
+        tv = TileValueBroadcast(B, src, device, group, n_groups)
+        from . import cusparse
+        C = cusparse._spgemm(A_block, B, alg=alg, chunk_fraction=chunk_fraction, by_tiles=tv)
+        tv.finish()
+        rowblock_step.last = tv
+        return C, B
     B, work = broadcast_csr(B_src, src, device, group, async_values=True)
     wait = work.wait if work is not None else (lambda: None)
     if multiply is not None:
         return multiply(A_block, B, wait), B
     return spgemm_rowblock(A_block, B, alg, chunk_fraction, before_numeric=wait), B
+
+
+rowblock_step.last = None
 
 
 def stitch_indptr(slab_indptrs, slab_nnz):

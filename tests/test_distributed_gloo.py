@@ -107,3 +107,84 @@ def test_product_prefix_matches_oracle():
     assert pref[0] == 0 and pref[-1] == oracle.num_products(Ah, Bh)
     for i in (0, 17, 199):
         assert pref[i + 1] - pref[i] == oracle.num_products(Ah[i:i + 1], Bh)
+
+
+def _tile_major(Bh, tw, G):
+    rows = np.repeat(np.arange(Bh.shape[0]), np.diff(Bh.indptr))
+    t = Bh.indices // tw
+    order = np.lexsort((np.arange(Bh.nnz), rows, t))
+    offs = np.zeros(G + 1, dtype=np.int64)
+    np.cumsum(np.bincount(t, minlength=G), out=offs[1:])
+    return Bh.data[order], offs
+
+
+def _tiles_worker(rank, world, port, out):
+    """TileValueBroadcast on gloo: the protocol of the pipelined values broadcast (the device
+    permutation and spg_numeric_tiles are the gpu tests'; here `tile_values` is numpy's)."""
+    import scipy.sparse as sp
+    import torch.distributed as dist
+    from spmm_amd import distributed
+    from spmm_amd.sparse import csr_matrix
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cpu = torch.device("cpu")
+    rng = np.random.default_rng(11)
+    Bh = sp.random(500, 1000, density=0.02, format="csr", random_state=rng)
+    Bh.sort_indices()
+    tw = 64
+    G = (1000 + tw - 1) // tw
+    tv, offs = _tile_major(Bh, tw, G)
+    B = distributed.broadcast_csr(csr_matrix(Bh, device=cpu) if rank == 0 else None, 0, cpu, values=False)
+    assert np.array_equal(B.indices.numpy(), Bh.indices)
+    geom = {"tile_width": tw, "tiles": G, "offsets": offs,
+            "tile_values": lambda: torch.from_numpy(tv.copy())}
+    bc = distributed.TileValueBroadcast(B, 0, cpu, n_groups=4)
+    tm, groups = bc(geom)
+    covered = []
+    for g0, g1 in groups:   # a group is released only once its slice has landed
+        a, b = int(offs[g0]), int(offs[g1])
+        ok = np.array_equal(tm[a:b].numpy(), tv[a:b]) or rank == 0
+        covered.append((g0, g1, ok))
+    bc.finish()
+    res = {"pipelined": bc.pipelined, "covered": covered, "full": bool(np.array_equal(tm.numpy(), tv))}
+    # disagreement (rank 1 plans another tile width) -> row-major values in one broadcast
+    B2 = distributed.broadcast_csr(csr_matrix(Bh, device=cpu) if rank == 0 else None, 0, cpu, values=False)
+    geom2 = dict(geom, tile_width=tw * (1 + rank))
+    bc2 = distributed.TileValueBroadcast(B2, 0, cpu)
+    res["fallback"] = bc2(geom2) is None and not bc2.pipelined
+    res["fallback_values"] = bool(np.array_equal(B2.data.numpy(), Bh.data))
+    # a rank without a tile plan (geom None) also sends everyone to the fallback
+    B3 = distributed.broadcast_csr(csr_matrix(Bh, device=cpu) if rank == 0 else None, 0, cpu, values=False)
+    bc3 = distributed.TileValueBroadcast(B3, 0, cpu)
+    res["fallback_none"] = bc3(geom if rank == 0 else None) is None
+    res["fallback_none_values"] = bool(np.array_equal(B3.data.numpy(), Bh.data))
+    out[rank] = res
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_tile_value_broadcast_gloo():
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_tiles_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    for r in range(world):
+        res = out[r]
+        assert res["pipelined"] and res["full"], (r, res)
+        assert [c[:2] for c in res["covered"]] == [c[:2] for c in out[0]["covered"]]
+        assert len(res["covered"]) == 4 and all(c[2] for c in res["covered"]), (r, res)
+        assert res["covered"][0][0] == 0 and res["covered"][-1][1] == 16
+        assert res["fallback"] and res["fallback_values"], (r, res)
+        assert res["fallback_none"] and res["fallback_none_values"], (r, res)
+
+
+def test_tile_groups_cover_and_balance():
+    from spmm_amd import distributed
+    offs = np.array([0, 10, 20, 30, 1000, 1010, 1020, 1030, 1040])
+    g = distributed.tile_groups(offs, 4)
+    assert g[0][0] == 0 and g[-1][1] == 8 and len(g) == 4
+    assert all(a < b for a, b in g) and all(g[i][1] == g[i + 1][0] for i in range(3))
+    assert distributed.tile_groups(offs, 100) == [(i, i + 1) for i in range(8)]
+    assert distributed.tile_groups(np.array([0, 5]), 8) == [(0, 1)]
+    assert distributed.tile_groups(np.array([0, 0, 0, 0]), 2) == [(0, 1), (1, 3)]

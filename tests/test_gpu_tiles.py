@@ -1,0 +1,206 @@
+"""The numeric phase by column-tile groups (spg_tile_value_offsets / spg_tile_values /
+spg_numeric_tiles, include/spgemm.h) -- the device half of the pipelined multi-GPU values
+broadcast (spmm_amd.distributed.TileValueBroadcast).
+
+* the tile-major order: offsets and permuted values equal a numpy restatement
+  (entries of column tile 0 row by row, then tile 1, ...) bit for bit;
+* groups: spg_numeric_tiles over consecutive tile ranges, fed values that did NOT come
+  from the plan's B (whose values are NaN here: the call must never read them), gives C
+  bit for bit as spgemm and as the oracle;
+* the fallback: plans off the tile path report no tile geometry and take spg_numeric;
+* a 2-rank rehearsal of rowblock_step(pipeline=True) on one GPU (gloo backend: RCCL
+  refuses two ranks on one device), stitched C bit-exact against the oracle.
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from oracle import oracle
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bits(x):
+    return x.view({4: np.uint32, 8: np.uint64, 16: np.uint64}[x.dtype.itemsize])
+
+
+def tile_major(B, tw, G):
+    """B's values in tile-major order and the G + 1 tile offsets (numpy restatement)."""
+    rows = np.repeat(np.arange(B.shape[0]), np.diff(B.indptr))
+    t = B.indices // tw
+    order = np.lexsort((np.arange(B.nnz), rows, t))
+    offs = np.zeros(G + 1, dtype=np.int64)
+    np.cumsum(np.bincount(t, minlength=G), out=offs[1:])
+    return B.data[order], offs
+
+
+def _canon(M):
+    M.sum_duplicates()
+    M.sort_indices()
+    return M
+
+
+def _cases():
+    """(name, A, B, alpha): the lean dense (2048-column) and sparse (8192-column) fp64 shapes,
+    config 3's, and f32 / complex128 tile plans."""
+    out = []
+    rng = np.random.default_rng(33)
+    A = sp.random(257, 17000, density=0.01, format="csr", random_state=rng, dtype=np.float64)
+    B = sp.random(17000, 17000, density=0.01, format="csr", random_state=rng, dtype=np.float64)
+    out.append(("dense2048_f64", A, B, 1.0))
+    rng = np.random.default_rng(34)
+    A = sp.random(300, 40000, density=0.0075, format="csr", random_state=rng)
+    B = sp.random(40000, 40000, density=0.00075, format="csr", random_state=rng)
+    out.append(("sparse8192_f64", A, B, 0.5))
+    from spmm_amd import gen
+    A, B = gen.scipy_pair(8192, 1e-2, seed=42)
+    out.append(("config3_f64", A, B, 1.0))
+    rng = np.random.default_rng(35)
+    A = sp.random(400, 20000, density=0.01, format="csr", random_state=rng, dtype=np.float32)
+    B = sp.random(20000, 20000, density=0.005, format="csr", random_state=rng, dtype=np.float32)
+    out.append(("f32", A, B, 2.0))
+    rng = np.random.default_rng(36)
+    A = sp.random(300, 12000, density=0.01, format="csr", random_state=rng).astype(np.complex128)
+    B = sp.random(12000, 12000, density=0.005, format="csr", random_state=rng).astype(np.complex128)
+    A.data = A.data + 1j * rng.standard_normal(A.nnz)
+    B.data = B.data + 1j * rng.standard_normal(B.nnz)
+    out.append(("c128", A, B, 1.0))
+    return [(n, _canon(a), _canon(b), al) for n, a, b, al in out]
+
+
+@pytest.mark.parametrize("case", [c[0] for c in _cases()])
+def test_numeric_by_tile_groups_bitexact(case):
+    from spmm_amd import cusparse, distributed
+    from spmm_amd.sparse import csr_matrix
+    name, A, B, alpha = next(c for c in _cases() if c[0] == case)
+    dA, dB = csr_matrix(A, device="cuda:0"), csr_matrix(B, device="cuda:0")
+    seen = {}
+
+    def probe(geom):   # the tile-major values as the plan lays them out
+        assert geom is not None, f"{name}: expected a tile plan with one chunk"
+        tv, offs = tile_major(B, geom["tile_width"], geom["tiles"])
+        assert np.array_equal(geom["offsets"], offs), f"{name}: tile offsets"
+        tm = geom["tile_values"]()
+        assert np.array_equal(_bits(tm.cpu().numpy()), _bits(tv)), f"{name}: tile-major values"
+        seen["geom"] = (geom["tile_width"], geom["tiles"])
+        return tm, distributed.tile_groups(offs, 1)
+
+    C0 = cusparse._spgemm(dA, dB, alpha=alpha, alg=2, by_tiles=probe)
+    ref = cusparse.spgemm(dA, dB, alpha=alpha, alg=2)
+    rp, rj, rx = oracle.spgemm(A, B, alpha=alpha, keep_zeros=True, sort=True, threads=16)
+    # values from outside the plan: B's own values NaN, the tile-major values from numpy
+    Bnan = B.copy()
+    Bnan.data[:] = np.nan
+    dBn = csr_matrix(Bnan, device="cuda:0")
+    G = seen["geom"][1]
+    for n_groups in (2, 5, G):
+        def feed(geom):
+            assert (geom["tile_width"], geom["tiles"]) == seen["geom"]
+            tv, offs = tile_major(B, geom["tile_width"], geom["tiles"])
+            return torch.from_numpy(tv).to("cuda:0"), distributed.tile_groups(offs, n_groups)
+        C = cusparse._spgemm(dA, dBn, alpha=alpha, alg=2, by_tiles=feed)
+        torch.cuda.synchronize()
+        for got in (C, C0):
+            assert np.array_equal(got.indptr.cpu().numpy().astype(np.int64), rp), (name, n_groups)
+            assert np.array_equal(got.indices.cpu().numpy(), rj), (name, n_groups)
+            assert np.array_equal(_bits(got.data.cpu().numpy()), _bits(rx)), (name, n_groups)
+        assert np.array_equal(_bits(C.data.cpu().numpy()), _bits(ref.data.cpu().numpy()))
+
+
+def test_numeric_tiles_fallback_off_tile_path():
+    """A product off the tile path (config 2's shape) reports no tile geometry; by_tiles
+    answers None and spg_numeric runs."""
+    from spmm_amd import cusparse
+    from spmm_amd.sparse import csr_matrix
+    rng = np.random.default_rng(5)
+    A = _canon(sp.random(2000, 2000, density=0.002, format="csr", random_state=rng))
+    B = _canon(sp.random(2000, 2000, density=0.002, format="csr", random_state=rng))
+    calls = []
+
+    def by_tiles(geom):
+        calls.append(geom)
+        return None
+
+    C = cusparse._spgemm(csr_matrix(A, device="cuda:0"), csr_matrix(B, device="cuda:0"), alg=2, by_tiles=by_tiles)
+    assert calls == [None]
+    rp, rj, rx = oracle.spgemm(A, B, keep_zeros=True, sort=True)
+    assert np.array_equal(C.indices.cpu().numpy(), rj)
+    assert np.array_equal(_bits(C.data.cpu().numpy()), _bits(rx))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+_REHEARSAL = r"""
+import os, sys, json
+import numpy as np, torch, torch.distributed as dist
+sys.path.insert(0, ROOT)
+from tests.test_gpu_tiles import _cases
+from spmm_amd import distributed
+from spmm_amd.sparse import csr_matrix
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+dist.init_process_group("gloo", rank=rank, world_size=world)
+dev = torch.device("cuda:0")
+out = {}
+for name, A, B, alpha in _cases():
+    if name not in ("sparse8192_f64", "dense2048_f64", "c128"):
+        continue
+    dA = csr_matrix(A, device=dev)
+    B_src = csr_matrix(B, device=dev) if rank == 0 else None
+    (r0, r1), A_blk, _ = distributed.rowblock_setup(dA, dA.indptr.new_tensor(B.indptr), world, rank)
+    C, _ = distributed.rowblock_step(A_blk, B_src, 0, dev, alg=2, pipeline=True, n_groups=3)
+    torch.cuda.synchronize()
+    tv = distributed.rowblock_step.last
+    np.savez(os.path.join(OUT, f"{name}_{rank}.npz"), p=C.indptr.cpu().numpy().astype(np.int64),
+             j=C.indices.cpu().numpy(), x=C.data.cpu().numpy(), rows=np.array([r0, r1]),
+             pipelined=np.array([tv.pipelined]), groups=np.array(tv.groups).reshape(-1, 2))
+dist.destroy_process_group()
+"""
+
+
+def test_pipelined_rowblock_two_ranks_one_gpu(tmp_path):
+    """rowblock_step(pipeline=True) with 2 ranks on cuda:0 (gloo): both plans agree on the
+    tile geometry, the values go as 3 tile groups, and the stitched C equals the oracle's
+    bit for bit."""
+    from spmm_amd import distributed
+    port = _free_port()
+    code = _REHEARSAL.replace("ROOT", repr(ROOT)).replace("OUT", repr(str(tmp_path)))
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-c", code], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    logs = []
+    for p in procs:
+        try:
+            logs.append(p.communicate(timeout=300)[0])
+        except subprocess.TimeoutExpired:
+            p.kill()
+            logs.append(p.communicate()[0])
+    assert all(p.returncode == 0 for p in procs), "\n".join(l[-3000:] for l in logs)
+    for name, A, B, alpha in _cases():
+        if name not in ("sparse8192_f64", "dense2048_f64", "c128"):
+            continue
+        parts = [np.load(tmp_path / f"{name}_{r}.npz") for r in range(2)]
+        assert all(bool(q["pipelined"][0]) for q in parts), name
+        assert all(len(q["groups"]) == 3 for q in parts), name
+        p = distributed.stitch_indptr([q["p"] for q in parts], [len(q["j"]) for q in parts])
+        j = np.concatenate([q["j"] for q in parts])
+        x = np.concatenate([q["x"] for q in parts])
+        rp, rj, rx = oracle.spgemm(A, B, keep_zeros=True, sort=True, threads=16)
+        assert np.array_equal(p, rp), name
+        assert np.array_equal(j, rj), name
+        assert np.array_equal(_bits(x), _bits(rx)), name
