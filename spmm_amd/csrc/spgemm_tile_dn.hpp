@@ -471,12 +471,15 @@ void k_tile_sp(
         const int w0 = min(nw, l * wpl), w1 = min(nw, w0 + wpl);
         uint32_t wd[SP_WPL] = {};
         int mine = 0;
-        if (SP_WPL == 4 && wpl == 4) {   // (8192-column tiles: a lane's 4 words in one 16-byte load)
-            const uint4 w4 = *reinterpret_cast<const uint4*>(ibits + w0);
-            wd[0] = w4.x;
-            wd[1 % SP_WPL] = w4.y;
-            wd[2 % SP_WPL] = w4.z;
-            wd[3 % SP_WPL] = w4.w;
+        if (SP_WPL % 4 == 0 && wpl == SP_WPL) {   // (widest tiles: a lane's words in 16-byte loads)
+#pragma unroll
+            for (int h = 0; h < SP_WPL / 4; ++h) {
+                const uint4 w4 = *reinterpret_cast<const uint4*>(ibits + w0 + 4 * h);
+                wd[(4 * h) % SP_WPL] = w4.x;
+                wd[(4 * h + 1) % SP_WPL] = w4.y;
+                wd[(4 * h + 2) % SP_WPL] = w4.z;
+                wd[(4 * h + 3) % SP_WPL] = w4.w;
+            }
 #pragma unroll
             for (int q = 0; q < SP_WPL; ++q) mine += __popc(wd[q]);
         } else {
