@@ -189,9 +189,6 @@ inline bool row_kernel_enabled() {
 #define SPG_TILE_LEAN 1
 #endif
 //   SPG_SP_LEAN     0 keeps the owner-round k_tile on sparse tiles (A/B against k_tile_sp)
-#ifndef SPG_SP16K
-#define SPG_SP16K 0   // (A/B: 16384-column sparse fp64 tiles, k_tile_sp<.., 4096>)
-#endif
 #ifndef SPG_SP_LEAN
 #define SPG_SP_LEAN 1
 #endif
@@ -245,12 +242,6 @@ inline bool want_tile(const spg_csr_t& A, const spg_csr_t& B, int& tws, int& G, 
     if (B.value_type == SPG_R_64F && lean && SPG_SP_LEAN && tws == 12 && frac >= 0.1 &&
         B.cols >= 16384 && frac * 8192.0 <= 0.95 * 2048)
         tws = 13;
-#if SPG_SP16K
-    // fp64 C rows up to 23 % dense: sparse tiles of 16384 columns in one 4096-slot window
-    if (B.value_type == SPG_R_64F && lean && SPG_SP_LEAN && tws == 13 && frac * 16384.0 <= 0.95 * 4096 &&
-        B.cols >= 32768)
-        tws = 14;
-#endif
     // (A/B timing builds only; at most 8192 columns: k_tile_sp<.., 2048> holds 256 bitmap words)
     if (SPG_TILE_TWS >= 8 && SPG_TILE_TWS <= 13) tws = SPG_TILE_TWS;
     if (frac * (double)(1 << tws) < 64.0) return false;
@@ -290,7 +281,7 @@ inline int sym_tile_log2(const spg_csr_t& B, int tws, bool* seg = nullptr) {
     if (seg_max >= SEG_MIN) return tmax;
     int t = tws;
     while (t < 16 && ((int64_t)1 << t) < B.cols && avgB * (double)((int64_t)1 << t) / (double)B.cols < 64.0) ++t;
-    return t;
+    return std::max(tws, std::min(t, SPG_SYM_MAXLOG));
 }
 
 
@@ -1052,10 +1043,6 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
                                           sent(2), it_lo, it_hi);   // (sparse tiles' region)
                 };
                 if constexpr (std::is_same<T, double>::value) {
-#if SPG_SP16K
-                    if (p.tws > 13) sp(std::integral_constant<int, 4096>{});
-                    else
-#endif
                     if (p.tws > 12) sp(std::integral_constant<int, 2048>{});
                     else sp(std::integral_constant<int, 1024>{});
                 } else {

@@ -473,8 +473,12 @@ struct __attribute__((aligned(16))) Sym8Ent {
     uint32_t wlen;   // words
     uint32_t lohi;   // (beg & 7) | (((beg + cnt - 1) & 7) + 1) << 8: valid halves of the first / last word
 };
+#ifndef SPG_SYM_MAXLOG
+#define SPG_SYM_MAXLOG 16   // (A/B: a narrower cap on the k_tile_sym8 tile, spgemm.hip sym_tile_log2)
+#endif
+constexpr int SYM8_NW = 1 << (SPG_SYM_MAXLOG - 5);   // k_tile_sym8 bitmap words (the widest tile)
 struct Sym8Lds {
-    uint32_t bits[SYM_NWMAX];
+    uint32_t bits[SYM8_NW];
     Sym8Ent ent[WAVE];
     uint8_t mk[TILE_MK];
 };

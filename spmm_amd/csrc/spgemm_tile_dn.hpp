@@ -421,7 +421,8 @@ __global__ __launch_bounds__(DN_WPB * WAVE) void k_tile_dn(
 // freed accumulator, and the column indices leave the same way.
 // The kernel is instantiated for two tile widths: up to 4096 columns (1024-slot windows, 128
 // bitmap words) and, fp64 only, 8192 columns (2048-slot windows, 256 words: config 5's
-// shape, numeric 128.7 -> 103.9 ms; 16384 columns measured 143 ms).
+// shape, numeric 128.7 -> 103.9 ms; 16384 columns measured 143 ms with 2048-slot windows and,
+// round 4, 138 ms with one 4096-slot window: 39 KB of LDS per wave leaves 4 waves per CU).
 template <int CAP> struct SpGeom {
     static constexpr int NWMAX = CAP / 8;          // bitmap words of the widest tile (TW = 4 * CAP)
     static constexpr int WPL = NWMAX / WAVE;       // bitmap words per lane (at most)

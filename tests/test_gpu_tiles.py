@@ -11,6 +11,7 @@ broadcast (spmm_amd.distributed.TileValueBroadcast).
 * a 2-rank rehearsal of rowblock_step(pipeline=True) on one GPU (gloo backend: RCCL
   refuses two ranks on one device), stitched C bit-exact against the oracle.
 """
+import functools
 import os
 import socket
 import subprocess
@@ -48,9 +49,11 @@ def _canon(M):
     return M
 
 
+@functools.lru_cache(maxsize=1)
 def _cases():
     """(name, A, B, alpha): the lean dense (2048-column) and sparse (8192-column) fp64 shapes,
-    config 3's, and f32 / complex128 tile plans."""
+    config 3's, one over three 65536-column symbolic blocks, and f32 / complex128 tile
+    plans (generated once per process)."""
     out = []
     rng = np.random.default_rng(33)
     A = sp.random(257, 17000, density=0.01, format="csr", random_state=rng, dtype=np.float64)
@@ -63,6 +66,10 @@ def _cases():
     from spmm_amd import gen
     A, B = gen.scipy_pair(8192, 1e-2, seed=42)
     out.append(("config3_f64", A, B, 1.0))
+    rng = np.random.default_rng(37)   # > 2 symbolic blocks of 65536 columns (wide symbolic tasks)
+    A = sp.random(200, 140000, density=7e-4, format="csr", random_state=rng)
+    B = sp.random(140000, 140000, density=7e-4, format="csr", random_state=rng)
+    out.append(("wide140k_f64", A, B, 1.0))
     rng = np.random.default_rng(35)
     A = sp.random(400, 20000, density=0.01, format="csr", random_state=rng, dtype=np.float32)
     B = sp.random(20000, 20000, density=0.005, format="csr", random_state=rng, dtype=np.float32)
