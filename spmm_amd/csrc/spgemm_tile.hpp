@@ -482,8 +482,11 @@ struct Sym8Lds {
     Sym8Ent ent[WAVE];
     uint8_t mk[TILE_MK];
 };
+#ifndef SPG_SYM8_WPE
+#define SPG_SYM8_WPE 1   // (A/B: a waves-per-SIMD floor for k_tile_sym8's register budget)
+#endif
 template <typename IP>
-__global__ __launch_bounds__(TILE_WPB * WAVE) void k_tile_sym8(
+__global__ __launch_bounds__(TILE_WPB * WAVE) __attribute__((amdgpu_waves_per_eu(SPG_SYM8_WPE))) void k_tile_sym8(
     int64_t row0, int64_t nrows, int tws, int G, int twss, const IP* __restrict__ Ap,
     const int32_t* __restrict__ Aj, const IP* __restrict__ Bp, const uint16_t* __restrict__ Bj16,
     const uint32_t* __restrict__ sidx, uint32_t* __restrict__ bitmap, int64_t* __restrict__ item_cnt) {
