@@ -128,7 +128,11 @@ def load():
             "spg_get_timing": (ctypes.c_int, [vp, ctypes.POINTER(SpgTiming)]),
         }
         for name, (res, args) in proto.items():
-            fn = getattr(lib, name)
+            fn = getattr(lib, name, None)
+            if fn is None:
+                if os.environ.get("SPG_LIB"):   # (an older development build: A/B timing only)
+                    continue
+                raise RuntimeError(f"{LIB_PATH} does not export {name}: rebuild it")
             fn.restype = res
             fn.argtypes = args
         _lib = lib
