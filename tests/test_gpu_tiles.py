@@ -162,16 +162,20 @@ rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
 dist.init_process_group("gloo", rank=rank, world_size=world)
 dev = torch.device("cuda:0")
 out = {}
-for name, A, B, alpha in _cases():
-    if name not in ("sparse8192_f64", "dense2048_f64", "c128"):
-        continue
+runs = [("sparse8192_f64", 2), ("dense2048_f64", 2), ("c128", 2),
+        ("dense2048_f64", 1),      # ALG1: no tile geometry -> the row-major values broadcast
+        ("sparse8192_f64", 3)]     # ALG3 with its chunks forced: several chunks -> the same
+cases = {c[0]: c for c in _cases()}
+for name, alg in runs:
+    _, A, B, alpha = cases[name]
+    os.environ["SPG_ALG3_CHUNK_ALWAYS"] = "1" if alg == 3 else "0"
     dA = csr_matrix(A, device=dev)
     B_src = csr_matrix(B, device=dev) if rank == 0 else None
     (r0, r1), A_blk, _ = distributed.rowblock_setup(dA, dA.indptr.new_tensor(B.indptr), world, rank)
-    C, _ = distributed.rowblock_step(A_blk, B_src, 0, dev, alg=2, pipeline=True, n_groups=3)
+    C, _ = distributed.rowblock_step(A_blk, B_src, 0, dev, alg=alg, pipeline=True, n_groups=3)
     torch.cuda.synchronize()
     tv = distributed.rowblock_step.last
-    np.savez(os.path.join(OUT, f"{name}_{rank}.npz"), p=C.indptr.cpu().numpy().astype(np.int64),
+    np.savez(os.path.join(OUT, f"{name}_alg{alg}_{rank}.npz"), p=C.indptr.cpu().numpy().astype(np.int64),
              j=C.indices.cpu().numpy(), x=C.data.cpu().numpy(), rows=np.array([r0, r1]),
              pipelined=np.array([tv.pipelined]), groups=np.array(tv.groups).reshape(-1, 2))
 dist.destroy_process_group()
@@ -180,8 +184,9 @@ dist.destroy_process_group()
 
 def test_pipelined_rowblock_two_ranks_one_gpu(tmp_path):
     """rowblock_step(pipeline=True) with 2 ranks on cuda:0 (gloo): both plans agree on the
-    tile geometry, the values go as 3 tile groups, and the stitched C equals the oracle's
-    bit for bit."""
+    tile geometry and the values go as 3 tile groups (ALG2), or both take the row-major
+    fallback (ALG1; ALG3 with several chunks); the stitched C equals the oracle's bit for
+    bit either way."""
     from spmm_amd import distributed
     port = _free_port()
     code = _REHEARSAL.replace("ROOT", repr(ROOT)).replace("OUT", repr(str(tmp_path)))
@@ -198,12 +203,15 @@ def test_pipelined_rowblock_two_ranks_one_gpu(tmp_path):
             p.kill()
             logs.append(p.communicate()[0])
     assert all(p.returncode == 0 for p in procs), "\n".join(l[-3000:] for l in logs)
-    for name, A, B, alpha in _cases():
-        if name not in ("sparse8192_f64", "dense2048_f64", "c128"):
-            continue
-        parts = [np.load(tmp_path / f"{name}_{r}.npz") for r in range(2)]
-        assert all(bool(q["pipelined"][0]) for q in parts), name
-        assert all(len(q["groups"]) == 3 for q in parts), name
+    cases = {c[0]: c for c in _cases()}
+    for name, alg in [("sparse8192_f64", 2), ("dense2048_f64", 2), ("c128", 2), ("dense2048_f64", 1),
+                      ("sparse8192_f64", 3)]:
+        _, A, B, alpha = cases[name]
+        parts = [np.load(tmp_path / f"{name}_alg{alg}_{r}.npz") for r in range(2)]
+        if alg == 2:   # pipelined: 3 tile groups on both ranks
+            assert all(bool(q["pipelined"][0]) and len(q["groups"]) == 3 for q in parts), (name, alg)
+        else:          # the fallback: one row-major values broadcast, spg_numeric
+            assert not any(bool(q["pipelined"][0]) for q in parts), (name, alg)
         p = distributed.stitch_indptr([q["p"] for q in parts], [len(q["j"]) for q in parts])
         j = np.concatenate([q["j"] for q in parts])
         x = np.concatenate([q["x"] for q in parts])
