@@ -123,10 +123,19 @@ template <typename T> __device__ __forceinline__ bool is_neg_zero(T v) {
     else return __float_as_uint(v) == 0x80000000u;
 }
 
+// Chunks (64 products) per marker group of the ordered walk (dn_walk), all of a group's
+// record loads in flight together: 16 for the widest kernels (2048-slot accumulators: LDS
+// holds them to 2 waves per SIMD, so the extra registers are free; round 4, config 4
+// numeric -2 %, config 5 -1 %), 8 for the 1024-slot ones (4 waves per SIMD at <= 128 VGPRs).
+#ifndef SPG_DN_U16
+#define SPG_DN_U16 1
+#endif
+__host__ __device__ constexpr int dn_mkb(int slots) { return (SPG_DN_U16 && slots >= 2048) ? 16 : 8; }
+
 template <typename T, int TWD, bool HIT = !dn_sent<T>()> struct DnLds {
     T acc[TWD + DN_DUMMY];        // accumulator by column; + the sentinel records' slots
     DnEnt<T> ent[WAVE + 1];
-    uint8_t mk[NUM_MK];           // lane -> A-entry markers of 8 chunks
+    uint8_t mk[dn_mkb(TWD) * WAVE];   // lane -> A-entry markers of one group's chunks
     uint8_t hit[TWD + DN_DUMMY];  // columns some product reached (non-sentinel types)
 };
 // (dn_sent, TWD 1024: 10,000 bytes per wave -- 8 two-wave blocks, 16 waves, fit a CU's 160 KB;
@@ -134,7 +143,7 @@ template <typename T, int TWD, bool HIT = !dn_sent<T>()> struct DnLds {
 template <typename T, int TWD> struct DnLds<T, TWD, false> {
     T acc[TWD + DN_DUMMY];
     DnEnt<T> ent[WAVE + 1];
-    uint8_t mk[NUM_MK];
+    uint8_t mk[dn_mkb(TWD) * WAVE];
 #ifdef SPG_LDS_PAD
     uint8_t pad[SPG_LDS_PAD];   // (A/B builds: occupancy sensitivity)
 #endif
@@ -142,17 +151,21 @@ template <typename T, int TWD> struct DnLds<T, TWD, false> {
 
 // Markers of one group of 8 chunks (transposed as num_group_markers): entry l's first product
 // gets l + 1, and product Pb (the batch's end, if inside the group) the pseudo entry's WAVE + 1.
+template <int MKB>
 __device__ __forceinline__ void dn_group_markers(uint8_t* mk, int l, int cnt, int off, int gb, int Pb) {
+    constexpr int SH = MKB == 16 ? 4 : 3;
+    constexpr int DN_MK = MKB * WAVE;
     wsync();
-    reinterpret_cast<uint2*>(mk)[l] = make_uint2(0u, 0u);
+    if constexpr (MKB == 16) reinterpret_cast<uint4*>(mk)[l] = make_uint4(0u, 0u, 0u, 0u);
+    else reinterpret_cast<uint2*>(mk)[l] = make_uint2(0u, 0u);
     wsync();
-    if (cnt > 0 && off >= gb && off < gb + NUM_MK) {
+    if (cnt > 0 && off >= gb && off < gb + DN_MK) {
         const int t = off - gb;
-        mk[((t & (WAVE - 1)) << 3) | (t >> 6)] = (uint8_t)(l + 1);
+        mk[((t & (WAVE - 1)) << SH) | (t >> 6)] = (uint8_t)(l + 1);
     }
-    if (l == 0 && Pb - gb < NUM_MK) {
+    if (l == 0 && Pb - gb < DN_MK) {
         const int t = Pb - gb;
-        mk[((t & (WAVE - 1)) << 3) | (t >> 6)] = (uint8_t)(WAVE + 1);
+        mk[((t & (WAVE - 1)) << SH) | (t >> 6)] = (uint8_t)(WAVE + 1);
     }
     wsync();
 }
@@ -163,12 +176,13 @@ __device__ __forceinline__ void dn_group_markers(uint8_t* mk, int l, int cnt, in
 // markers; per U chunks the lane -> entry max-scans, one 16-byte table read and one record load
 // per chunk (all in flight), then per chunk in order one multiply and one ds_add_f64 into
 // acc[slot(column)] and hit(slot).  `sent` is the byte offset of the kernel's sentinel region.
-template <typename T, int NB, typename L, typename Slot, typename Hit>
+template <typename T, int NB, int MKB, typename L, typename Slot, typename Hit>
 __device__ __forceinline__ void dn_walk(L* lp, T* acc, int l, const int32_t* __restrict__ tp, int64_t a0, int nA,
                                         T (&aq)[NB], uint2 (&sq)[NB], const int32_t* __restrict__ Aj,
                                         const T* __restrict__ Ax, const char* __restrict__ rb, uint32_t sent,
                                         Slot&& slot, Hit&& hit) {
-    constexpr int U = sizeof(T) > 8 ? 4 : 8;     // chunks in flight
+    constexpr int U = (sizeof(T) > 8 ? 4 : 8) * (MKB / 8);   // chunks in flight
+    constexpr int DN_MK = MKB * WAVE;                         // products per marker group
     constexpr uint32_t RB = (uint32_t)rec_bytes<T>();   // bytes of one B record
     DnEnt<T>* ent = lp->ent;
     uint8_t* mk = lp->mk;
@@ -204,19 +218,30 @@ __device__ __forceinline__ void dn_walk(L* lp, T* acc, int l, const int32_t* __r
             ent[WAVE].a = (T)0;
         }
         unsigned carry = 0u;
-        for (int gb = 0; gb < Pb; gb += NUM_MK) {
-            dn_group_markers(mk, l, cnt, off, gb, Pb);
-            const int nchg = min(NUM_MK, Pb - gb);
-            const uint2 m2 = reinterpret_cast<const uint2*>(mk)[l];
-            const uint64_t mrow = ((uint64_t)m2.y << 32) | m2.x;
+        for (int gb = 0; gb < Pb; gb += DN_MK) {
+            dn_group_markers<MKB>(mk, l, cnt, off, gb, Pb);
+            const int nchg = min(DN_MK, Pb - gb);
+            uint64_t mrow[MKB / 8];   // this lane's marker byte of each chunk of the group
+            if constexpr (MKB == 16) {
+                const uint4 m4 = reinterpret_cast<const uint4*>(mk)[l];
+                mrow[0] = ((uint64_t)m4.y << 32) | m4.x;
+                mrow[(MKB / 8) - 1] = ((uint64_t)m4.w << 32) | m4.z;
+            } else {
+                const uint2 m2 = reinterpret_cast<const uint2*>(mk)[l];
+                mrow[0] = ((uint64_t)m2.y << 32) | m2.x;
+            }
             for (int c0 = 0; c0 < nchg; c0 += U * WAVE) {
                 const int nu = min(U, (nchg - c0 + WAVE - 1) >> 6);
                 auto step = [&](auto nuc) {
                     constexpr int NU = decltype(nuc)::value;
-                    const uint64_t mb = mrow >> (8 * (c0 >> 6));
+                    const int cb = c0 >> 6;   // first chunk of the step (0 when U covers the group)
                     unsigned sp[NU];
 #pragma unroll
-                    for (int u = 0; u < NU; ++u) sp[u] = wave_incl_umax_dpp((unsigned)(mb >> (8 * u)) & 0xffu);
+                    for (int u = 0; u < NU; ++u) {
+                        const int i = cb + u;
+                        const uint64_t w = (MKB == 16 && i >= 8) ? mrow[(MKB / 8) - 1] : mrow[0];
+                        sp[u] = wave_incl_umax_dpp((unsigned)(w >> (8 * (i & 7))) & 0xffu);
+                    }
 #pragma unroll
                     for (int u = 0; u < NU; ++u) {
                         sp[u] = max(sp[u], carry);
@@ -356,7 +381,7 @@ __device__ __forceinline__ void dn_item(DnLds<T, TWD>& S, int l, int TW, int lo,
                                         int32_t* __restrict__ crow,
                                         T* __restrict__ xrow, T alpha) {
     dn_clear(S, l, TW);
-    dn_walk<T, NB>(&S, S.acc, l, tp, a0, nA, aq, sq, Aj, Ax, rb, sent, [&](int c) { return c; },
+    dn_walk<T, NB, dn_mkb(TWD)>(&S, S.acc, l, tp, a0, nA, aq, sq, Aj, Ax, rb, sent, [&](int c) { return c; },
                    [&](int c) {
                        if constexpr (!dn_sent<T>()) S.hit[c] = 1;
                    });
@@ -431,7 +456,7 @@ template <typename T, int CAP> struct SpLds {
     T acc[CAP + WAVE];            // compact accumulator of one window; + lane-private slots
     uint2 bw[SpGeom<CAP>::NWMAX];   // (bitmap word, popcount prefix)
     DnEnt<T> ent[WAVE + 1];
-    uint8_t mk[NUM_MK];
+    uint8_t mk[dn_mkb(CAP) * WAVE];
 #ifdef SPG_LDS_PAD
     uint8_t pad[SPG_LDS_PAD];   // (A/B builds: occupancy sensitivity)
 #endif
@@ -537,7 +562,7 @@ void k_tile_sp(
             wsync();
             for (int p = l; p < wn; p += WAVE) S.acc[p] = (T)0;
             if (L0 > 0) preload();   // (the walk consumes the queue; rare later windows reload it)
-            dn_walk<T, NB>(&S, S.acc, l, tp, a0, nA, aq, sq, Aj, Ax, rb, sent,
+            dn_walk<T, NB, dn_mkb(SP_CAP)>(&S, S.acc, l, tp, a0, nA, aq, sq, Aj, Ax, rb, sent,
                            [&](int rc) -> int {
                                if (rc < clo || rc >= chi) return SP_CAP + l;   // (sentinels too)
                                const uint2 b = S.bw[rc >> 5];
