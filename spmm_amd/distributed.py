@@ -7,7 +7,7 @@ cross-GPU reduction.  The collectives are
 * ``broadcast_csr``: B from ``src`` to every rank: one 6-int64 metadata broadcast (the
   reference's sparse broadcast protocol, modify_src/cupy-src/cupyx/distributed/
   _nccl_comm.py:651-674, metadata exchange :506-530), then the structure (row pointer and
-  column indices packed into ONE buffer) and the values (a second buffer), each a single
+  column indices packed into ONE buffer; 16-bit columns when B is at most 65536 wide) and the values (a second buffer), each a single
   RCCL broadcast -- the reference groups its three payload broadcasts between
   groupStart/groupEnd (:669); two packed buffers are the same "few large collectives" on
   torch.distributed.  With ``async_values=True`` the values broadcast is left in flight and
@@ -65,9 +65,15 @@ def broadcast_csr(M: csr_matrix | None, src: int, device, group=None, async_valu
     rows, cols, nnz, dtc, ipc, _ = (int(x) for x in meta.tolist())
     ipt = _CODE_IP[ipc]
     ib = torch.empty(0, dtype=ipt).element_size()
-    sbytes = ib * (rows + 1) + 4 * nnz          # structure: indptr | indices
+    # column indices of a matrix at most 65536 wide travel as their low 16 bits (exact), half
+    # the structure bytes -- the part of the step's broadcast the symbolic pass waits for
+    cb = 2 if cols <= 65536 else 4
+    sbytes = ib * (rows + 1) + cb * nnz          # structure: indptr | indices
     if rank == src:
-        struct = torch.cat([_bytes_of(M.indptr.to(device)), _bytes_of(M.indices.to(device))])
+        idx = M.indices.to(device).contiguous()
+        if cb == 2:
+            idx = idx.view(torch.int16)[0::2].contiguous()   # (little-endian: the low halves)
+        struct = torch.cat([_bytes_of(M.indptr.to(device)), _bytes_of(idx)])
         data = M.data.to(device).contiguous()
     else:
         struct = torch.empty(sbytes, dtype=torch.uint8, device=device)
@@ -80,7 +86,12 @@ def broadcast_csr(M: csr_matrix | None, src: int, device, group=None, async_valu
         else:
             dist.broadcast(_bytes_of(data), src, group=group)
     indptr = struct[:ib * (rows + 1)].view(ipt)
-    indices = struct[ib * (rows + 1):].view(torch.int32)
+    if rank == src:
+        indices = M.indices.to(device)
+    elif cb == 2:
+        indices = struct[ib * (rows + 1):].view(torch.int16).to(torch.int32) & 0xffff
+    else:
+        indices = struct[ib * (rows + 1):].view(torch.int32)
     out = csr_matrix._from_parts(data, indices, indptr, (rows, cols), canonical=True)
     return (out, work) if async_values else out
 

@@ -188,3 +188,35 @@ def test_tile_groups_cover_and_balance():
     assert distributed.tile_groups(offs, 100) == [(i, i + 1) for i in range(8)]
     assert distributed.tile_groups(np.array([0, 5]), 8) == [(0, 1)]
     assert distributed.tile_groups(np.array([0, 0, 0, 0]), 2) == [(0, 1), (1, 3)]
+
+
+def _wide_worker(rank, world, port, out):
+    """broadcast_csr on both structure encodings: 16-bit columns (B at most 65536 wide) and
+    32-bit ones (wider), each received exactly."""
+    import scipy.sparse as sp
+    import torch.distributed as dist
+    from spmm_amd import distributed
+    from spmm_amd.sparse import csr_matrix
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cpu = torch.device("cpu")
+    ok = []
+    for cols in (65536, 65537, 200000):
+        rng = np.random.default_rng(cols)
+        Bh = sp.random(40, cols, density=40.0 / cols, format="csr", random_state=rng)
+        Bh.indices[-1] = cols - 1 if Bh.nnz else 0   # the widest column travels too
+        Bh.sort_indices()
+        B = distributed.broadcast_csr(csr_matrix(Bh, device=cpu) if rank == 0 else None, 0, cpu)
+        ok.append(bool(np.array_equal(B.indices.numpy(), Bh.indices) and np.array_equal(B.indptr.numpy(), Bh.indptr)
+                       and np.array_equal(B.data.numpy(), Bh.data) and B.indices.dtype == torch.int32))
+    out[rank] = ok
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_broadcast_csr_column_encodings_gloo():
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_wide_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    assert out[0] == [True] * 3 and out[1] == [True] * 3, dict(out)
