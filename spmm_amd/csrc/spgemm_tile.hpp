@@ -490,10 +490,7 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) __attribute__((amdgpu_waves_per_eu
     int64_t row0, int64_t nrows, int tws, int G, int twss, const IP* __restrict__ Ap,
     const int32_t* __restrict__ Aj, const IP* __restrict__ Bp, const uint16_t* __restrict__ Bj16,
     const uint32_t* __restrict__ sidx, uint32_t* __restrict__ bitmap, int64_t* __restrict__ item_cnt) {
-#ifndef SPG_SYM8_U
-#define SPG_SYM8_U 8
-#endif
-    constexpr int U = SPG_SYM8_U;   // chunks of 64 words in flight
+    constexpr int U = 8;   // chunks of 64 words in flight
     __shared__ __attribute__((aligned(16))) Sym8Lds lds[TILE_WPB];
     const int l = lane_id();
     const int wv = uniform((int)(threadIdx.x >> 6));
@@ -556,7 +553,6 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) __attribute__((amdgpu_waves_per_eu
                 const uint4 mrow = reinterpret_cast<const uint4*>(S.mk)[l];
                 for (int c0 = 0; c0 < nchg; c0 += U * WAVE) {
                     const uint64_t mb = marker_bytes(mrow, c0 >> 6);
-                    const uint64_t mb2 = U > 8 ? marker_bytes(mrow, (c0 >> 6) + 8) : 0;   // (chunks 8..15)
                     uint4 w[U];
                     uint32_t lo[U], hi[U];
 #pragma unroll
@@ -566,8 +562,7 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) __attribute__((amdgpu_waves_per_eu
                         w[u] = make_uint4(0u, 0u, 0u, 0u);
                         const int cc = c0 + u * WAVE;
                         if (cc < nchg) {
-                            const uint64_t mbu = u < 8 ? mb : mb2;
-                            const unsigned sp = max(wave_incl_umax_dpp((unsigned)(mbu >> (8 * (u & 7))) & 0xffu), carry);
+                            const unsigned sp = max(wave_incl_umax_dpp((unsigned)(mb >> (8 * u)) & 0xffu), carry);
                             carry = (unsigned)readlane_i((int)sp, WAVE - 1);
                             const int t = gb + cc + l;
                             if (t < Wb) {

@@ -637,10 +637,7 @@ __global__ __launch_bounds__(SEG_WPB * WAVE) void k_tile_sym_seg(
     int64_t row0, int64_t nrows, int tws, int G, int twss, const IP* __restrict__ Ap,
     const int32_t* __restrict__ Aj, const IP* __restrict__ Bp, const uint16_t* __restrict__ Bj16,
     const uint32_t* __restrict__ sidx, uint32_t* __restrict__ bitmap, int64_t* __restrict__ item_cnt) {
-#ifndef SPG_SEG_NQ
-#define SPG_SEG_NQ 4
-#endif
-    constexpr int NQ = SPG_SEG_NQ;   // quads of A entries per round: 16 entries, 4 loads in flight per lane
+    constexpr int NQ = 4;   // quads of A entries per round: 16 entries, 4 loads in flight per lane
     __shared__ __attribute__((aligned(16))) uint32_t bits_all[SEG_WPB][SYM_NWMAX];
     const int l = lane_id();
     const int sub = l & 15, grp = l >> 4;
