@@ -219,3 +219,32 @@ def test_pipelined_rowblock_two_ranks_one_gpu(tmp_path):
         assert np.array_equal(p, rp), name
         assert np.array_equal(j, rj), name
         assert np.array_equal(_bits(x), _bits(rx)), name
+
+
+def test_numeric_tiles_argument_errors():
+    """spg_numeric_tiles rejects a range past the last tile (SPG_STATUS_INVALID_VALUE), and the
+    shim rejects groups that skip or leave out tiles."""
+    from spmm_amd import _lib, cusparse
+    from spmm_amd.sparse import csr_matrix
+    name, A, B, alpha = next(c for c in _cases() if c[0] == "dense2048_f64")
+    dA, dB = csr_matrix(A, device="cuda:0"), csr_matrix(B, device="cuda:0")
+
+    def past_end(geom):
+        return geom["tile_values"](), [(0, geom["tiles"] + 1)]
+
+    with pytest.raises(_lib.SpgError) as e:
+        cusparse._spgemm(dA, dB, alg=2, by_tiles=past_end)
+    assert e.value.status == 3   # SPG_STATUS_INVALID_VALUE
+
+    def gap(geom):
+        return geom["tile_values"](), [(0, 1), (2, geom["tiles"])]
+
+    with pytest.raises(RuntimeError, match="consecutive"):
+        cusparse._spgemm(dA, dB, alg=2, by_tiles=gap)
+
+    def short(geom):
+        return geom["tile_values"](), [(0, geom["tiles"] - 1)]
+
+    with pytest.raises(RuntimeError, match="covered"):
+        cusparse._spgemm(dA, dB, alg=2, by_tiles=short)
+    torch.cuda.synchronize()
