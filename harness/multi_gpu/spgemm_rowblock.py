@@ -10,8 +10,9 @@ Launch:  python -m torch.distributed.run --nproc-per-node G --master-addr 127.0.
   and rank r keeps the rows [r0, r1) cut on the product-count prefix (equal products per
   rank, spmm_amd.distributed.rowblock_setup);
 * a timed step is spmm_amd.distributed.rowblock_step: B broadcast from rank 0 (metadata, one
-  packed structure buffer, the values left in flight through the symbolic pass) and this
-  rank's slab; GFLOPS = sum_r 2 P_r / max_r t_r; the broadcast alone is timed beside it;
+  packed structure buffer, then the values in tile-major groups, each group's numeric tiles
+  launched as it lands -- or, if a plan cannot run by tiles, one values broadcast left in
+  flight through the symbolic pass) and this rank's slab; GFLOPS = sum_r 2 P_r / max_r t_r; the broadcast alone is timed beside it;
   allgather of the per-rank nnz gives the global row-pointer offsets;
 * --check S: S sampled rows per rank are recomputed on the host with the CPU oracle
   (tests/ oracle, parity check only) and compared bit for bit.
