@@ -91,6 +91,7 @@ def main():
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
+        C = None   # (the previous slab is freed before the next one is built)
         C, B = step()
     torch.cuda.synchronize()
     t = time.perf_counter() - t0
@@ -105,7 +106,8 @@ def main():
         rng = np.random.default_rng(rank)
         rows = np.sort(rng.choice(r1 - r0, size=min(args.check, r1 - r0), replace=False))
         Ah = A.get()[rows]
-        Bh = B.get()
+        # (after a pipelined step B's values are row-major on rank 0 only: fetch them whole)
+        Bh = (distributed.broadcast_csr(B0 if rank == 0 else None, 0, dev) if world > 1 else B).get()
         ref = oracle.spgemm(sp.csr_matrix(Ah), Bh, keep_zeros=True, sort=True)
         cp = C.indptr.cpu().numpy().astype(np.int64)
         for q, i in enumerate(rows):
