@@ -76,10 +76,16 @@ def _csr_view(m: csr_matrix) -> SpgCsr:
                   _IT[m.indptr.dtype], _VT[m.data.dtype])
 
 
+def _current_stream_ptr(dev: int) -> int:
+    raw = getattr(torch._C, "_cuda_getCurrentRawStream", None)   # (no Stream object per call)
+    return raw(dev) if raw is not None else torch.cuda.current_stream(dev).cuda_stream
+
+
 def _handle_for(m: csr_matrix) -> _lib.Handle:
-    dev = m.device.index if m.device.index is not None else torch.cuda.current_device()
+    d = m.device
+    dev = d.index if d.index is not None else torch.cuda.current_device()
     h = _lib.get_handle(dev)
-    h.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    h.set_stream(_current_stream_ptr(dev))
     return h
 
 
@@ -94,7 +100,12 @@ def validate_csr(m: csr_matrix) -> int:
     return res.value
 
 
+_VALUE_DTYPES = (torch.float32, torch.float64, torch.complex64, torch.complex128)
+
+
 def _cast_common_type(a: csr_matrix, b: csr_matrix):
+    if a.data.dtype is b.data.dtype and a.data.dtype in _VALUE_DTYPES:   # (the per-call common case)
+        return a, b
     dt = np.promote_types(a.dtype, b.dtype)
     if dt not in (np.float32, np.float64, np.complex64, np.complex128):
         raise TypeError(f"spgemm supports float32/float64/complex64/complex128, got {dt}")
