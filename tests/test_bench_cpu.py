@@ -70,6 +70,9 @@ def test_bench_spawns_ranks_without_launcher(tmp_path, world):
     assert len(lines) == 1, r.stdout
     line = json.loads(lines[0])
     assert line["n_gpus"] == world and line["steps"] == 2 and line["warmup"] == 1
+    # the pipelined-broadcast report is a GPU figure: present, and None on the CPU hook path
+    assert "b_values_pipeline" in line and line["b_values_pipeline"] is None
+    assert "b_values_pipeline" in line["config5"] and line["config5"]["b_values_pipeline"] is None
     assert line["scaling"] == "weak" and line["config"]["rows_per_rank"] == n
     assert line["config5"]["scaling"] == "strong"
 
