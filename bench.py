@@ -213,7 +213,10 @@ def cpu_baseline(A_h, B_h, rows_sample, budget_s):
             "port": {"gflops": round(2.0 * P / t_port / 1e9, 4), "ms_per_run": round(t_port * 1e3, 3),
                      "threads": 1, "what": "oracle/gustavson.c (scipy's rule restated in C)"},
             "omp": {"gflops": round(2.0 * P / t_omp / 1e9, 4), "ms_per_run": round(t_omp * 1e3, 3),
-                    "threads": nthr, "what": "oracle/gustavson.c, OpenMP over rows"},
+                    "threads": nthr, "what": "oracle/gustavson.c, OpenMP over rows",
+                    "thread_cap": (f"OMP_NUM_THREADS={os.environ['OMP_NUM_THREADS']}: the CPU share this job gets "
+                                   f"on the GPU box (os.cpu_count()={os.cpu_count()} counts the whole host)")
+                    if os.environ.get("OMP_NUM_THREADS") else "all host CPUs"},
             "host_cpus": os.cpu_count()}
 
 
@@ -254,9 +257,16 @@ class Ctx:
             self.dev = torch.device("cuda", self.local_dev)
         else:
             self.local_dev, self.dev = None, torch.device("cpu")
+        self.backend = None
         if self.world > 1:
             backend = os.environ.get("SPG_DIST_BACKEND", "nccl" if self.gpu else "gloo")   # nccl = RCCL
             dist.init_process_group(backend, **({"device_id": self.dev} if backend == "nccl" else {}))
+            self.backend = backend
+
+    def collective_name(self):
+        """The collective library the broadcasts actually ran on (the line must not claim RCCL
+        for a gloo rehearsal)."""
+        return {"nccl": "RCCL", "gloo": "gloo (host-staged; a rehearsal, not xGMI)"}.get(self.backend, self.backend)
 
     def sync(self):
         if self.gpu:
@@ -429,7 +439,8 @@ def run_config4(ctx, args, cfg, tdt, vb, hook):
             f"{alg3_label(alg, nch)}, chunk_fraction {cf}")
     if w > 1:
         desc += (f"; weak scaling: rank r owns rows [r*{n}, (r+1)*{n}) of a {w * n}x{n} A "
-                 "(rank 0's block is the N=1 A), B broadcast over RCCL inside every step, no reduction")
+                 f"(rank 0's block is the N=1 A), B broadcast over {ctx.collective_name()} inside every step, "
+                 "no reduction")
     out = {
         "value": round(2.0 * P_all * steps / elapsed / 1e9, 3), "steps": steps, "warmup": warmup,
         "ms_per_step": round(ms, 5), "scaling": "weak",
@@ -438,7 +449,8 @@ def run_config4(ctx, args, cfg, tdt, vb, hook):
                    "alg3_cap": None if alg != 3 else ("binding" if nch > 1 else "not binding"),
                    "nnzB": int(nnzB), "nnzA_rank0" if w > 1 else "nnzA": int(A.nnz),
                    "nnzC": int(nnz_all), "num_products": int(P_all),
-                   "parallelism": "single GPU" if w == 1 else f"row-block x{w} (weak), B broadcast over RCCL"},
+                   "parallelism": "single GPU" if w == 1 else
+                   f"row-block x{w} (weak), B broadcast over {ctx.collective_name()}"},
         "peak_hbm_bytes": int(peak_max), "roofline": rf,
         "phases_ms_per_step": {k: round(v[0] / reps, 5) for k, v in ph.items() if v[1]},
         "b_broadcast_ms": None if bcast_ms is None else round(bcast_ms, 3),
@@ -570,7 +582,7 @@ def run_config5(ctx, args, cfg, n, tdt, vb, hook, steps, warmup):
            "workload": (f"{cfg['name']}: random CSR {n}x{n} density={dens:g} {args.dtype}, ALG{alg}; "
                         f"{w} row blocks cut on the product prefix (each rank draws its own block), "
                         f"{alg3_label(alg, nch)}, "
-                        "B broadcast over RCCL inside every step")}
+                        + ("one GPU" if w == 1 else f"B broadcast over {ctx.collective_name()} inside every step"))}
     del A, B
     return out
 
@@ -602,7 +614,10 @@ def run_alg3_chunked(ctx, args, tdt, n=262144, dens=1e-3, cf=0.02, steps=2, warm
         key = "alg2" if alg == 2 else "alg3"
         out[key] = {"chunk_fraction": c, "n_chunks": nch, "ms_per_step": round(elapsed / steps * 1e3, 3),
                     "gflops": round(2.0 * P * steps / elapsed / 1e9, 3),
-                    "peak_hbm_bytes": int(cusparse.last_stats.peak_bytes)}
+                    "peak_hbm_bytes": int(cusparse.last_stats.peak_bytes),
+                    # the working set ALG3 caps (peak minus C's own arrays): the figure comparable
+                    # to the reference's ALG1 -> ALG3 trade (6.03 -> 2.44 GB)
+                    "workspace_bytes": int(cusparse.last_stats.workspace_bytes)}
         # the same C under both schedules: position-weighted sums of the arrays on the device,
         # in pieces (no 190 GB copy to the host, no int64 copy of all of C)
         torch = ctx.torch
@@ -614,6 +629,7 @@ def run_alg3_chunked(ctx, args, tdt, n=262144, dens=1e-3, cf=0.02, steps=2, warm
         torch.cuda.empty_cache()
     out["alg3_over_alg2_time"] = round(out["alg3"]["ms_per_step"] / out["alg2"]["ms_per_step"], 3)
     out["alg3_over_alg2_peak"] = round(out["alg3"]["peak_hbm_bytes"] / out["alg2"]["peak_hbm_bytes"], 3)
+    out["alg3_over_alg2_workspace"] = round(out["alg3"]["workspace_bytes"] / max(1, out["alg2"]["workspace_bytes"]), 4)
     del A, B
     return out
 

@@ -287,11 +287,12 @@ typedef enum {
     SPG_PHASE_COMPACT = 4,    /* k_compact: ALG1 copy into C                        */
     SPG_PHASE_VALIDATE = 5,   /* k_validate                                         */
     SPG_PHASE_SPILL = 6,      /* k_symbolic / k_numeric over the rows the short-row */
-                              /* kernel handed on (list mode); the tile path's      */
-                              /* once-per-plan builds (k_tile_index, k_bt_count,     */
-                              /* k_bj16, k_bt_pack)                                  */
+                              /* kernel handed on (list mode)                        */
     SPG_PHASE_SPMV = 7,       /* k_spmv                                             */
-    SPG_NUM_PHASES = 8
+    SPG_PHASE_LAYOUT = 8,     /* the tile path's B re-layout: once per plan          */
+                              /* (k_tile_index, k_bt_count, k_bj16, k_bt_pack) and   */
+                              /* per tile group (k_bt_fill, spg_numeric_tiles)        */
+    SPG_NUM_PHASES = 9
 } spg_phase_t;
 
 typedef struct {

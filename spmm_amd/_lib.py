@@ -48,8 +48,8 @@ EXPORTS = ("spg_version", "spg_build_info", "spg_status_string", "spg_create", "
            "spg_spgemm_ws", "spg_plan_info", "spg_tile_value_offsets", "spg_tile_values",
            "spg_numeric_tiles")
 
-PHASES = ("products", "scan", "symbolic", "numeric", "compact", "validate", "spill", "spmv")
-NUM_PHASES = 8
+PHASES = ("products", "scan", "symbolic", "numeric", "compact", "validate", "spill", "spmv", "b_layout")
+NUM_PHASES = 9
 
 
 class SpgCsr(ctypes.Structure):

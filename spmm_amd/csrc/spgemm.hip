@@ -883,15 +883,15 @@ spg_status_t tile_build_index(spg_handle_t h, spg_plan_s& p) {
     const int32_t* Bj = (const int32_t*)p.B.indices;
     const int R = 1 << (p.twss - p.tws);
     {
-        timed_launch(h, SPG_PHASE_SPILL, k_tile_index<IP>, dim3((unsigned)grid_for(p.B.rows, 4)), dim3(256), p.B.rows,
+        timed_launch(h, SPG_PHASE_LAYOUT, k_tile_index<IP>, dim3((unsigned)grid_for(p.B.rows, 4)), dim3(256), p.B.rows,
                      Bp, Bj, p.tws, p.G, p.tidx);
         SPG_LAUNCHED(h);
         const int64_t n2 = p.B.rows * p.G + p.G;
-        timed_launch(h, SPG_PHASE_SPILL, k_bt_count,
+        timed_launch(h, SPG_PHASE_LAYOUT, k_bt_count,
                      dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(grid_for(n2, 256), 65536))), dim3(256),
                      p.B.rows, p.G, R, (const uint2*)p.tidx, p.tptr, p.sidx);
         SPG_LAUNCHED(h);
-        timed_launch(h, SPG_PHASE_SPILL, k_bj16,
+        timed_launch(h, SPG_PHASE_LAYOUT, k_bj16,
                      dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(grid_for(p.B.nnz, 256), 65536))), dim3(256),
                      p.B.nnz, Bj, p.bj16);
         SPG_LAUNCHED(h);
@@ -983,7 +983,7 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
     const T* Bx = (const T*)p.B.values;
     if (tm) {
         if (!p.brec_cols) {
-            timed_launch(h, SPG_PHASE_SPILL, k_bt_pack<T, IP, 1>, dim3((unsigned)grid_for(p.B.rows, 4)), dim3(256),
+            timed_launch(h, SPG_PHASE_LAYOUT, k_bt_pack<T, IP, 1>, dim3((unsigned)grid_for(p.B.rows, 4)), dim3(256),
                          p.B.rows, Bp, Bj, Bx, p.tws, (const int32_t*)p.tptr, (uint32_t*)p.brec, p.B.nnz, (T*)nullptr);
             SPG_LAUNCHED(h);
             p.brec_cols = true;
@@ -994,12 +994,12 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
         const int32_t* tp = (const int32_t*)p.tptr;
         const int64_t K1 = p.B.rows + 1;
         const int64_t est = std::max<int64_t>(1, p.B.nnz * (g1 - g0) / std::max<int64_t>(p.G, 1));
-        timed_launch(h, SPG_PHASE_SPILL, k_bt_fill<T>,
+        timed_launch(h, SPG_PHASE_LAYOUT, k_bt_fill<T>,
                      dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(grid_for(est, 256), 16384))), dim3(256),
                      tp + g0 * K1, tp + (g1 - 1) * K1 + p.B.rows, tm, (uint32_t*)p.brec);
         SPG_LAUNCHED(h);
     } else if (!p.brec_built) {
-        timed_launch(h, SPG_PHASE_SPILL, k_bt_pack<T, IP>, dim3((unsigned)grid_for(p.B.rows, 4)), dim3(256), p.B.rows,
+        timed_launch(h, SPG_PHASE_LAYOUT, k_bt_pack<T, IP>, dim3((unsigned)grid_for(p.B.rows, 4)), dim3(256), p.B.rows,
                      Bp, Bj, Bx, p.tws, (const int32_t*)p.tptr, (uint32_t*)p.brec, p.B.nnz, (T*)nullptr);
         SPG_LAUNCHED(h);
         p.brec_built = true;
@@ -1732,7 +1732,7 @@ spg_status_t spg_tile_values(spg_handle_t h, spg_plan_t p, void* tm) {
         using T = decltype(tag);
         auto go = [&](auto ip) {
             using IP = decltype(ip);
-            timed_launch(h, SPG_PHASE_SPILL, k_bt_pack<T, IP, 2>, dim3((unsigned)grid_for(p->B.rows, 4)), dim3(256),
+            timed_launch(h, SPG_PHASE_LAYOUT, k_bt_pack<T, IP, 2>, dim3((unsigned)grid_for(p->B.rows, 4)), dim3(256),
                          p->B.rows, (const IP*)p->B.indptr, (const int32_t*)p->B.indices, (const T*)p->B.values,
                          p->tws, (const int32_t*)p->tptr, (uint32_t*)p->brec, p->B.nnz, (T*)tm);
         };

@@ -141,7 +141,7 @@ def _spgemm(a, b, alpha=1, alg=0, chunk_fraction=0.2, verbose=False, before_nume
     run by tiles (not the tile path, several row chunks, ALG1); then `by_tiles` makes
     b.data complete and returns None, and spg_numeric runs.  Otherwise geom is a dict
     (tile_width, tiles, offsets: the tiles + 1 tile-major value offsets, tile_values(): B's
-    values permuted tile-major by this plan) and `by_tiles` returns (tm, groups): the
+    values permuted tile-major by this plan, dtype: the plan's value type) and `by_tiles` returns (tm, groups): the
     tile-major values tensor and an iterable of (tile_begin, tile_end) ranges, each yielded
     once its slice of tm is ready on the current stream, together covering every tile."""
     if not check_availability("spgemm"):
@@ -253,7 +253,9 @@ def _numeric_by_tiles(h, plan, b, al, vc, by_tiles) -> bool:
     info = _lib.SpgPlanInfo()
     check(lib.spg_plan_info(plan, ctypes.byref(info), None, 0), "spg_plan_info")
     geom = None
-    if info.path == 2 and info.n_chunks == 1:
+    # (a development library built without the tile-group entry points: spg_numeric)
+    has_tiles = all(hasattr(lib, f) for f in ("spg_tile_value_offsets", "spg_tile_values", "spg_numeric_tiles"))
+    if has_tiles and info.path == 2 and info.n_chunks == 1:
         G = int(info.tiles_per_row)
         offs = (ctypes.c_int64 * (G + 1))()
         st = lib.spg_tile_value_offsets(h.ptr, plan, offs, G + 1)
@@ -263,7 +265,7 @@ def _numeric_by_tiles(h, plan, b, al, vc, by_tiles) -> bool:
                 check(lib.spg_tile_values(h.ptr, plan, ctypes.c_void_p(tm.data_ptr())), "spg_tile_values")
                 return tm[:b.nnz]
             geom = {"tile_width": int(info.tile_width), "tiles": G, "offsets": np.frombuffer(offs, dtype=np.int64).copy(),
-                    "tile_values": tile_values}
+                    "tile_values": tile_values, "dtype": b.data.dtype}
         elif st != _lib.STATUS_NOT_SUPPORTED:
             check(st, "spg_tile_value_offsets")
     got = by_tiles(geom)

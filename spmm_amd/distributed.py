@@ -200,14 +200,14 @@ def tile_groups(offsets, n_groups: int):
 
 
 def agree_tiles(geom, device, group=None) -> bool:
-    """Every rank's plan runs by tiles with the same tile width and count (one 3-int64
-    all_gather; a collective every rank calls once per step)."""
+    """Every rank's plan runs by tiles with the same tile width, tile count and value type
+    (one 4-int64 all_gather; a collective every rank calls once per step)."""
     world = dist.get_world_size(group)
     if dist.get_backend(group) != "nccl":
         device = "cpu"   # gloo (the rehearsal on one GPU) gathers host tensors
-    mine = torch.tensor([1, geom["tile_width"], geom["tiles"]] if geom is not None else [0, 0, 0],
-                        dtype=torch.int64, device=device)
-    out = [torch.zeros(3, dtype=torch.int64, device=device) for _ in range(world)]
+    mine = torch.tensor([1, geom["tile_width"], geom["tiles"], _DT_CODE[geom["dtype"]]] if geom is not None
+                        else [0, 0, 0, -1], dtype=torch.int64, device=device)
+    out = [torch.zeros(4, dtype=torch.int64, device=device) for _ in range(world)]
     dist.all_gather(out, mine, group=group)
     rows = [tuple(int(v) for v in t.tolist()) for t in out]
     return rows[0][0] == 1 and all(r == rows[0] for r in rows)
@@ -239,7 +239,8 @@ class TileValueBroadcast:
         if rank == self.src:
             tm = geom["tile_values"]()
         else:
-            tm = torch.empty(self.B.nnz, dtype=self.B.data.dtype, device=self.device)
+            # the plan's value type, which every rank agreed on (agree_tiles), not the buffer's
+            tm = torch.empty(self.B.nnz, dtype=geom["dtype"], device=self.device)
         self.groups = tile_groups(offs, self.n_groups)
         works = []
         for g0, g1 in self.groups:
@@ -256,10 +257,25 @@ class TileValueBroadcast:
             yield g0, g1
 
     def finish(self):
-        for w in self.works:
+        """Order the current stream after every outstanding broadcast (also after a failed
+        multiply: peers must not be left blocked in a group broadcast) and drop the
+        references to B and its values."""
+        works, self.works = self.works, []
+        for w in works:
             if w is not None:
                 w.wait()
-        self.works = []
+        self.B = None
+
+    def report(self):
+        """(pipelined, groups) of the step, for the bench line (no tensors kept alive)."""
+        return StepReport(self.pipelined, list(self.groups))
+
+
+class StepReport:
+    """What the last rowblock_step did (rowblock_step.last): only report fields."""
+
+    def __init__(self, pipelined: bool, groups):
+        self.pipelined, self.groups = pipelined, groups
 
 
 def rowblock_step(A_block: csr_matrix, B_src: csr_matrix | None, src: int, device, alg: int = 2,
@@ -270,20 +286,38 @@ def rowblock_step(A_block: csr_matrix, B_src: csr_matrix | None, src: int, devic
     rank's slab A_block . B.  `multiply(A_block, B, wait_values)` replaces the device
     multiply (the gloo tests run the CPU oracle there).  `pipeline` (default: on a GPU
     device): the values travel tile-major in `n_groups` async broadcasts, each group's
-    numeric tiles starting as its slice lands (TileValueBroadcast).  Returns (C slab, B);
-    after a pipelined step B's values are row-major on `src` only."""
+    numeric tiles starting as its slice lands (TileValueBroadcast).
+
+    Returns (C slab, B).  After a pipelined step B's values exist row-major on `src` only,
+    so the other ranks get None for B (their B never held row-major values).  A_block is
+    cast to B's value type when that type is the common one; otherwise (B would have to be
+    promoted after its values arrive) the step takes the row-major values broadcast."""
     if pipeline is None:
         pipeline = multiply is None and torch.device(device).type == "cuda"
     if pipeline and multiply is None:
         B, _ = broadcast_csr(B_src, src, device, group, async_values=True, values=False)
-        tv = TileValueBroadcast(B, src, device, group, n_groups)
-        from . import cusparse
-        C = cusparse._spgemm(A_block, B, alg=alg, chunk_fraction=chunk_fraction, by_tiles=tv)
-        tv.finish()
-        rowblock_step.last = tv
-        return C, B
+        if A_block.data.dtype != B.data.dtype:
+            common = np.promote_types(A_block.dtype, B.dtype)
+            if common == B.dtype:
+                A_block = A_block.astype(common)
+        if A_block.data.dtype == B.data.dtype:
+            tv = TileValueBroadcast(B, src, device, group, n_groups)
+            from . import cusparse
+            try:
+                C = cusparse._spgemm(A_block, B, alg=alg, chunk_fraction=chunk_fraction, by_tiles=tv)
+            finally:
+                tv.finish()
+            rowblock_step.last = tv.report()
+            rank = dist.get_rank(group)
+            return C, (B if (rank == src or not tv.pipelined) else None)
+        # mixed value types that promote B: the values row-major, then the shim promotes both
+        if B.nnz:
+            dist.broadcast(_bytes_of(B.data), src, group=group)
+        rowblock_step.last = StepReport(False, [])
+        return spgemm_rowblock(A_block, B, alg, chunk_fraction), B
     B, work = broadcast_csr(B_src, src, device, group, async_values=True)
     wait = work.wait if work is not None else (lambda: None)
+    rowblock_step.last = StepReport(False, [])
     if multiply is not None:
         return multiply(A_block, B, wait), B
     return spgemm_rowblock(A_block, B, alg, chunk_fraction, before_numeric=wait), B

@@ -137,7 +137,7 @@ def _tiles_worker(rank, world, port, out):
     tv, offs = _tile_major(Bh, tw, G)
     B = distributed.broadcast_csr(csr_matrix(Bh, device=cpu) if rank == 0 else None, 0, cpu, values=False)
     assert np.array_equal(B.indices.numpy(), Bh.indices)
-    geom = {"tile_width": tw, "tiles": G, "offsets": offs,
+    geom = {"tile_width": tw, "tiles": G, "offsets": offs, "dtype": torch.float64,
             "tile_values": lambda: torch.from_numpy(tv.copy())}
     bc = distributed.TileValueBroadcast(B, 0, cpu, n_groups=4)
     tm, groups = bc(geom)
@@ -159,6 +159,11 @@ def _tiles_worker(rank, world, port, out):
     bc3 = distributed.TileValueBroadcast(B3, 0, cpu)
     res["fallback_none"] = bc3(geom if rank == 0 else None) is None
     res["fallback_none_values"] = bool(np.array_equal(B3.data.numpy(), Bh.data))
+    # plans of different value types (the ranks would send different byte counts)
+    B4 = distributed.broadcast_csr(csr_matrix(Bh, device=cpu) if rank == 0 else None, 0, cpu, values=False)
+    bc4 = distributed.TileValueBroadcast(B4, 0, cpu)
+    res["fallback_dtype"] = bc4(dict(geom, dtype=torch.float64 if rank == 0 else torch.float32)) is None
+    res["fallback_dtype_values"] = bool(np.array_equal(B4.data.numpy(), Bh.data))
     out[rank] = res
     dist.barrier()
     dist.destroy_process_group()
@@ -177,6 +182,7 @@ def test_tile_value_broadcast_gloo():
         assert res["covered"][0][0] == 0 and res["covered"][-1][1] == 16
         assert res["fallback"] and res["fallback_values"], (r, res)
         assert res["fallback_none"] and res["fallback_none_values"], (r, res)
+        assert res["fallback_dtype"] and res["fallback_dtype_values"], (r, res)
 
 
 def test_tile_groups_cover_and_balance():
