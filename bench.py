@@ -364,7 +364,9 @@ def tile_kernel(ctx, A, B, alg, cf):
     nch = len(info["chunk_rows"]) - 1
     if info["path"] != "tile":
         return info["path"], nch
-    return ("k_tile_dn" if info["dense_tiles"] else "k_tile_sp") + f" (TW={info['tile_width']}, {nch} chunk(s))", nch
+    rg = info.get("record_group", 1)
+    return (("k_tile_dn" if info["dense_tiles"] else "k_tile_sp") + f" (TW={info['tile_width']}"
+            + (f", cooperative record groups of {rg} tiles" if rg > 1 else "") + f", {nch} chunk(s))"), nch
 
 
 def alg3_label(alg, nch):

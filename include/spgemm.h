@@ -216,7 +216,10 @@ spg_status_t spg_validate_csr(spg_handle_t handle, const spg_csr_t *M, int *is_c
  * `capacity` entries written; chunk_rows may be NULL when capacity is 0).  lds_ordered 1
  * when fp64 / complex128 tiles run the ordered-LDS-add kernels -- the handle's device check at
  * spg_create found the ordering they rely on -- and 0 when they fall back to owner rounds
- * (same results). */
+ * (same results).  record_group (tile path): numeric tiles per VALUE TILE -- B's records are
+ * laid out per group of that many adjacent tiles (1: plain tile-major); the value-tile API
+ * below works in value tiles of tile_width * record_group columns, ceil(tiles_per_row /
+ * record_group) of them. */
 typedef struct {
     int path;
     int tile_width;
@@ -224,6 +227,7 @@ typedef struct {
     int dense_tiles;
     int64_t n_chunks;
     int lds_ordered;
+    int record_group;
 } spg_plan_info_t;
 spg_status_t spg_plan_info(spg_plan_t plan, spg_plan_info_t *info, int64_t *chunk_rows, int64_t capacity);
 
@@ -256,16 +260,20 @@ spg_status_t spg_spgemm_ws(spg_handle_t handle, const spg_csr_t *A, const spg_cs
  * _nccl_comm.py:651-674; no cuSPARSE counterpart: cusparseSpGEMM_compute needs all of B).
  * Tile-path plans with one row chunk only (spg_plan_info: path 2, n_chunks 1); anything
  * else returns SPG_STATUS_NOT_SUPPORTED and the caller takes spg_numeric.
- *   spg_tile_value_offsets: the plan's tiles_per_row + 1 offsets (entries) of each column
- *     tile's values in TILE-MAJOR order -- B's entries with columns in tile 0 row by row,
- *     then tile 1, ...  One device->host copy.  The order depends only on B's structure
- *     and the tile width, so plans on different devices with equal tile widths agree.
+ * The unit is the VALUE TILE: record_group adjacent numeric tiles (spg_plan_info), i.e. a
+ * column range of tile_width * record_group columns; value_tiles = ceil(tiles_per_row /
+ * record_group).
+ *   spg_tile_value_offsets: the value_tiles + 1 offsets (entries) of each value tile's
+ *     values in TILE-MAJOR order -- B's entries with columns in value tile 0 row by row,
+ *     then value tile 1, ...  One device->host copy.  The order depends only on B's
+ *     structure and the value-tile width, so plans on different devices with equal widths
+ *     agree.
  *   spg_tile_values: B's values (row-major, B->values of the plan) permuted into that
  *     order (nnz(B) entries of B's value type) -- on the device that holds them.
- *   spg_numeric_tiles: C's entries in columns of tiles [tile_begin, tile_end) from the
+ *   spg_numeric_tiles: C's entries in columns of value tiles [tile_begin, tile_end) from the
  *     tile-major values (only that range of them is read), after spg_symbolic, stream-
- *     ordered like spg_numeric.  Calls over disjoint ranges covering every tile give C
- *     bit for bit as spg_numeric does; the plan's B->values is never read. */
+ *     ordered like spg_numeric.  Calls over disjoint ranges covering every value tile give
+ *     C bit for bit as spg_numeric does; the plan's B->values is never read. */
 spg_status_t spg_tile_value_offsets(spg_handle_t handle, spg_plan_t plan, int64_t *offsets, int64_t capacity);
 spg_status_t spg_tile_values(spg_handle_t handle, spg_plan_t plan, void *tile_major_values);
 spg_status_t spg_numeric_tiles(spg_handle_t handle, spg_plan_t plan, const void *alpha, spg_csr_t *C,

@@ -63,12 +63,13 @@ class SpgCsr(ctypes.Structure):
 class SpgPlanInfo(ctypes.Structure):
     """spg_plan_info_t"""
     _fields_ = [("path", ctypes.c_int), ("tile_width", ctypes.c_int), ("tiles_per_row", ctypes.c_int64),
-                ("dense_tiles", ctypes.c_int), ("n_chunks", ctypes.c_int64), ("lds_ordered", ctypes.c_int)]
+                ("dense_tiles", ctypes.c_int), ("n_chunks", ctypes.c_int64), ("lds_ordered", ctypes.c_int),
+                ("record_group", ctypes.c_int)]
 
 
 class SpgTiming(ctypes.Structure):
     """spg_timing_t"""
-    _fields_ = [("ms", ctypes.c_double * 8), ("launches", ctypes.c_int64 * 8)]
+    _fields_ = [("ms", ctypes.c_double * NUM_PHASES), ("launches", ctypes.c_int64 * NUM_PHASES)]
 
 
 class SpgError(RuntimeError):

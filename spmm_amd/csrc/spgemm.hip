@@ -91,6 +91,8 @@ struct spg_plan_s {
     int tws = 10;                   // log2 of the tile width
     int G = 1;                      // tiles per row
     int TR = 1;                     // tiles per wave task (a run of one row's tiles)
+    int rgs = 0;                    // log2 of the tiles per record group (tile-major B's layout: RG
+                                    // adjacent tiles' segments of a B row side by side)
     int twss = 10;                  // log2 of the symbolic tile width (>= tws, <= 16)
     bool sym_seg = false;           // symbolic tiles by the segment-walking kernel (long segments)
     bool counts_ready = false;      // a symbolic pass has completed (counts / offsets valid)
@@ -585,7 +587,25 @@ inline int64_t* tile_chunk_items(const spg_plan_s& p, int64_t c) {
     return tile_dense(p) ? p.item_cnt + tile_chunk_r0(p, c) * p.G : p.item_cnt;
 }
 inline int sym_tiles(const spg_plan_s& p) { const int R = 1 << (p.twss - p.tws); return (p.G + R - 1) / R; }
-inline int64_t bt_entries(const spg_plan_s& p) { return p.use_tile ? (int64_t)p.G * (p.B.rows + 1) : 0; }
+// record groups of the tile-major B: Gq groups of RG = 1 << rgs tiles (the last padded to RG)
+inline int64_t rec_groups(const spg_plan_s& p) { return ((int64_t)p.G + (1 << p.rgs) - 1) >> p.rgs; }
+inline int64_t tiles_padded(const spg_plan_s& p) { return rec_groups(p) << p.rgs; }
+inline int64_t group_words(const spg_plan_s& p) { return (p.B.rows << p.rgs) + 1; }   // one group's table
+inline int64_t bt_entries(const spg_plan_s& p) { return p.use_tile ? rec_groups(p) * group_words(p) : 0; }
+// fp64 8192-column sparse tiles (config 5's shape) run in cooperative record groups of
+// 1 << SPG_SP_RGS tiles (k_tile_sp<.., RG>); every other tile plan keeps RG = 1
+#ifndef SPG_SP_RGS
+#define SPG_SP_RGS 2
+#endif
+// (SPG_SP_RECORD_GROUP=1, read per plan: a schedule-only switch to the one-wave kernel over
+// plain tile-major records, for A/B timing and for the tests; results are identical)
+inline int record_group_log2(const spg_plan_s& p) {
+    if (!p.use_tile || tile_dense(p) || !p.lean || !SPG_SP_LEAN) return 0;
+    if (p.A.value_type != SPG_R_64F || p.tws != 13) return 0;
+    const char* e = std::getenv("SPG_SP_RECORD_GROUP");
+    if (e && std::strcmp(e, "1") == 0) return 0;
+    return SPG_SP_RGS;
+}
 
 // ALG1 runs as one fused pass (k_short SHORT_NUMLB) when the short-row kernel takes the shape
 inline bool fused_alg1(const spg_plan_s& p) {
@@ -625,7 +645,7 @@ Layout make_layout(const spg_plan_s& p) {
         // item bitmaps; before the first symbolic pass the region holds the row-major
         // boundary index the tile-major B is built from
         const size_t bm = tile_dense(p) ? 0 : sizeof(uint32_t) * (size_t)tile_items(p) * (size_t)((1 << p.tws) >> 5);
-        const size_t ti = sizeof(uint2) * (size_t)p.B.rows * (size_t)p.G;
+        const size_t ti = sizeof(uint2) * (size_t)p.B.rows * (size_t)tiles_padded(p);
         L.bitmap = off; off = align_up(off + std::max(bm, ti));
     }
     if (p.alg == SPG_ALG1 && !p.use_tile) {
@@ -883,13 +903,14 @@ spg_status_t tile_build_index(spg_handle_t h, spg_plan_s& p) {
     const int32_t* Bj = (const int32_t*)p.B.indices;
     const int R = 1 << (p.twss - p.tws);
     {
+        const int Gp = (int)tiles_padded(p);
         timed_launch(h, SPG_PHASE_LAYOUT, k_tile_index<IP>, dim3((unsigned)grid_for(p.B.rows, 4)), dim3(256), p.B.rows,
-                     Bp, Bj, p.tws, p.G, p.tidx);
+                     Bp, Bj, p.tws, Gp, p.tidx);
         SPG_LAUNCHED(h);
-        const int64_t n2 = p.B.rows * p.G + p.G;
+        const int64_t n2 = p.B.rows * Gp + rec_groups(p);
         timed_launch(h, SPG_PHASE_LAYOUT, k_bt_count,
                      dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(grid_for(n2, 256), 65536))), dim3(256),
-                     p.B.rows, p.G, R, (const uint2*)p.tidx, p.tptr, p.sidx);
+                     p.B.rows, Gp, p.G, R, (const uint2*)p.tidx, p.tptr, p.sidx, p.rgs);
         SPG_LAUNCHED(h);
         timed_launch(h, SPG_PHASE_LAYOUT, k_bj16,
                      dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(grid_for(p.B.nnz, 256), 65536))), dim3(256),
@@ -984,23 +1005,25 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
     if (tm) {
         if (!p.brec_cols) {
             timed_launch(h, SPG_PHASE_LAYOUT, k_bt_pack<T, IP, 1>, dim3((unsigned)grid_for(p.B.rows, 4)), dim3(256),
-                         p.B.rows, Bp, Bj, Bx, p.tws, (const int32_t*)p.tptr, (uint32_t*)p.brec, p.B.nnz, (T*)nullptr);
+                         p.B.rows, Bp, Bj, Bx, p.tws, (const int32_t*)p.tptr, (uint32_t*)p.brec, p.B.nnz, (T*)nullptr,
+                         p.rgs);
             SPG_LAUNCHED(h);
             p.brec_cols = true;
         }
         p.brec_built = false;   // values of other tiles are stale for a later spg_numeric
-        // records [tptr[g0][0], tptr[g1-1][K]) (the tile-major table is one scan: tile g's
-        // records start where tile g-1's end)
+        // records of groups [q0, q1) = [table word q0*W, word (q1-1)*W + W-1) -- the table is one
+        // scan: group q's records start where group q-1's end (g0 and g1 are group-aligned)
         const int32_t* tp = (const int32_t*)p.tptr;
-        const int64_t K1 = p.B.rows + 1;
-        const int64_t est = std::max<int64_t>(1, p.B.nnz * (g1 - g0) / std::max<int64_t>(p.G, 1));
+        const int64_t W = group_words(p);
+        const int64_t q0 = g0 >> p.rgs, q1 = (g1 + (1 << p.rgs) - 1) >> p.rgs;
+        const int64_t est = std::max<int64_t>(1, p.B.nnz * (q1 - q0) / std::max<int64_t>(rec_groups(p), 1));
         timed_launch(h, SPG_PHASE_LAYOUT, k_bt_fill<T>,
                      dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(grid_for(est, 256), 16384))), dim3(256),
-                     tp + g0 * K1, tp + (g1 - 1) * K1 + p.B.rows, tm, (uint32_t*)p.brec);
+                     tp + q0 * W, tp + (q1 - 1) * W + (W - 1), tm, (uint32_t*)p.brec);
         SPG_LAUNCHED(h);
     } else if (!p.brec_built) {
         timed_launch(h, SPG_PHASE_LAYOUT, k_bt_pack<T, IP>, dim3((unsigned)grid_for(p.B.rows, 4)), dim3(256), p.B.rows,
-                     Bp, Bj, Bx, p.tws, (const int32_t*)p.tptr, (uint32_t*)p.brec, p.B.nnz, (T*)nullptr);
+                     Bp, Bj, Bx, p.tws, (const int32_t*)p.tptr, (uint32_t*)p.brec, p.B.nnz, (T*)nullptr, p.rgs);
         SPG_LAUNCHED(h);
         p.brec_built = true;
         p.brec_cols = true;
@@ -1015,9 +1038,10 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
         if (nch > 1 && !tile_dense(p) && (st = tile_sym_chunk<IP>(h, p, c))) return st;
         const int64_t r0 = tile_chunk_r0(p, c), n = tile_chunk_r1(p, c) - r0;
         if (n <= 0) continue;
-        // the items of tiles [g0, g1) (host keeps rows*G < 2^31)
-        const uint32_t it_lo = (uint32_t)(g0 * n), it_hi = (uint32_t)(g1 * n);
-        const int64_t nit = (g1 - g0) * n;
+        // the items of tiles [g0, g1) (host keeps rows*G < 2^31); items of record groups
+        // [g0 / RG, ceil(g1 / RG)) for the cooperative sparse kernel
+        uint32_t it_lo = (uint32_t)(g0 * n), it_hi = (uint32_t)(g1 * n);
+        int64_t nit = (g1 - g0) * n;
         KernelTimer kt(h, SPG_PHASE_NUMERIC);
         // dense accumulator when the tile fits one window; round groups (tile_variant())
         const bool dense = tile_dense(p);
@@ -1030,23 +1054,33 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
                                   h->stream, kt.a, kt.b, 0, r0, n, p.tws, p.G, Ap, Aj, Ax, p.B.rows,
                                   (const uint32_t*)p.brec, (const int32_t*)p.tptr,
                                   dense ? (const uint32_t*)nullptr : (const uint32_t*)p.bitmap,
-                                  (const int64_t*)tile_chunk_items(p, c), cj, cx, alpha, it_lo, it_hi);
+                                  (const int64_t*)tile_chunk_items(p, c), cj, cx, alpha, it_lo, it_hi, p.rgs);
         };
         if constexpr (OrderedLdsAdd<T>::value) {
             if (!dense && p.lean && SPG_SP_LEAN) {   // sparse tiles, ordered LDS adds
-                auto sp = [&](auto capc) {
-                    constexpr int CAP = decltype(capc)::value;
-                    hipExtLaunchKernelGGL((k_tile_sp<T, IP, CAP>), dim3(tile_grid(nit, SP_WPB)), dim3(SP_WPB * WAVE),
+                auto sp = [&](auto cfg, auto rgc) {
+                    using CF = decltype(cfg);
+                    constexpr int RG = decltype(rgc)::value;
+                    if (RG > 1) {   // items (record group, row): one block of RG waves each
+                        const int64_t q0 = g0 >> p.rgs, q1 = (g1 + RG - 1) >> p.rgs;
+                        it_lo = (uint32_t)(q0 * n);
+                        it_hi = (uint32_t)(q1 * n);
+                        nit = (q1 - q0) * n;
+                    }
+                    hipExtLaunchKernelGGL((k_tile_sp<T, IP, CF, RG>), dim3(tile_grid(nit, 1)), dim3(RG * WAVE),
                                           0, h->stream, kt.a, kt.b, 0, r0, n, p.tws, p.G, Ap, Aj, Ax, p.B.rows,
                                           (const uint32_t*)p.brec, (const int32_t*)p.tptr, (const uint32_t*)p.bitmap,
                                           (const int64_t*)tile_chunk_items(p, c), cj, cx, alpha,
-                                          sent(2), it_lo, it_hi);   // (sparse tiles' region)
+                                          sent(2), it_lo, it_hi, p.rgs);   // (sparse tiles' region)
                 };
+                using One = std::integral_constant<int, 1>;
                 if constexpr (std::is_same<T, double>::value) {
-                    if (p.tws > 12) sp(std::integral_constant<int, 2048>{});
-                    else sp(std::integral_constant<int, 1024>{});
+                    if (p.tws > 12 && p.rgs == SPG_SP_RGS && SPG_SP_RGS > 0)
+                        sp(SpCfgRG{}, std::integral_constant<int, (1 << SPG_SP_RGS)>{});
+                    else if (p.tws > 12) sp(SpCfg2048{}, One{});
+                    else sp(SpCfg1024{}, One{});
                 } else {
-                    sp(std::integral_constant<int, 1024>{});
+                    sp(SpCfg1024{}, One{});
                 }
                 SPG_LAUNCHED(h);
                 continue;
@@ -1058,7 +1092,7 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
                                           0, h->stream, kt.a, kt.b, 0, r0, n, p.tws, p.G, Ap, Aj, Ax, p.B.rows,
                                           (const uint32_t*)p.brec, (const int32_t*)p.tptr,
                                           (const int64_t*)tile_chunk_items(p, c), cj, cx, alpha,
-                                          sent(sentinel_region(TWD)), it_lo, it_hi);
+                                          sent(sentinel_region(TWD)), it_lo, it_hi, p.rgs);
                 };
                 if constexpr (std::is_same<T, double>::value) {
                     if ((1 << p.tws) > 1024) dn(std::integral_constant<int, 2048>{});
@@ -1371,6 +1405,7 @@ spg_status_t spg_plan(spg_handle_t h, const spg_csr_t* A, const spg_csr_t* B, sp
     if (tmp.use_tile) {
         tmp.TR = 1;
         tmp.twss = sym_tile_log2(*B, tmp.tws, &tmp.sym_seg);
+        tmp.rgs = record_group_log2(tmp);
     }
     // spills are rare for the shapes the short kernel is chosen for (A rows > 64 entries or
     // C wider than 16384 columns): a small grid keeps the usually-empty launch cheap
@@ -1703,18 +1738,19 @@ spg_status_t spg_tile_value_offsets(spg_handle_t h, spg_plan_t p, int64_t* offse
     if (!h) return SPG_STATUS_NOT_INITIALIZED;
     spg_status_t st = tiles_supported(p);
     if (st) return st;
-    if (capacity < p->G + 1 || !offsets) return SPG_STATUS_INVALID_VALUE;
+    const int64_t Gq = rec_groups(*p);   // value tiles = record groups
+    if (capacity < Gq + 1 || !offsets) return SPG_STATUS_INVALID_VALUE;
     DeviceGuard dg_(h->device);
     SPG_HIP(h, dg_.err);
-    // tile g starts at table word g*(K+1); the last tile's end slot holds nnz(B)
-    const int64_t K1 = p->B.rows + 1;
-    std::vector<int32_t> w((size_t)p->G + 1);
-    SPG_HIP(h, hipMemcpy2DAsync(w.data(), sizeof(int32_t), p->tptr, (size_t)K1 * sizeof(int32_t), sizeof(int32_t),
-                                (size_t)p->G, hipMemcpyDeviceToHost, h->stream));
-    SPG_HIP(h, hipMemcpyAsync(w.data() + p->G, (const int32_t*)p->tptr + (p->G - 1) * K1 + p->B.rows,
+    // group q starts at table word q*W; the last group's end slot holds nnz(B)
+    const int64_t W = group_words(*p);
+    std::vector<int32_t> w((size_t)Gq + 1);
+    SPG_HIP(h, hipMemcpy2DAsync(w.data(), sizeof(int32_t), p->tptr, (size_t)W * sizeof(int32_t), sizeof(int32_t),
+                                (size_t)Gq, hipMemcpyDeviceToHost, h->stream));
+    SPG_HIP(h, hipMemcpyAsync(w.data() + Gq, (const int32_t*)p->tptr + (Gq - 1) * W + (W - 1),
                               sizeof(int32_t), hipMemcpyDeviceToHost, h->stream));
     SPG_HIP(h, hipStreamSynchronize(h->stream));
-    for (int64_t g = 0; g <= p->G; ++g) offsets[g] = w[(size_t)g];
+    for (int64_t g = 0; g <= Gq; ++g) offsets[g] = w[(size_t)g];
     return SPG_STATUS_SUCCESS;
 }
 
@@ -1734,7 +1770,7 @@ spg_status_t spg_tile_values(spg_handle_t h, spg_plan_t p, void* tm) {
             using IP = decltype(ip);
             timed_launch(h, SPG_PHASE_LAYOUT, k_bt_pack<T, IP, 2>, dim3((unsigned)grid_for(p->B.rows, 4)), dim3(256),
                          p->B.rows, (const IP*)p->B.indptr, (const int32_t*)p->B.indices, (const T*)p->B.values,
-                         p->tws, (const int32_t*)p->tptr, (uint32_t*)p->brec, p->B.nnz, (T*)tm);
+                         p->tws, (const int32_t*)p->tptr, (uint32_t*)p->brec, p->B.nnz, (T*)tm, p->rgs);
         };
         if (i64) go(int64_t{}); else go(int32_t{});
         SPG_LAUNCHED(h);
@@ -1749,7 +1785,7 @@ spg_status_t spg_numeric_tiles(spg_handle_t h, spg_plan_t p, const void* alpha, 
     if (p->nnzC < 0) return SPG_STATUS_NOT_INITIALIZED;     // spg_symbolic first
     spg_status_t st = tiles_supported(p);
     if (st) return st;
-    if (g0 < 0 || g1 > p->G || g0 > g1) return SPG_STATUS_INVALID_VALUE;
+    if (g0 < 0 || g1 > rec_groups(*p) || g0 > g1) return SPG_STATUS_INVALID_VALUE;   // value tiles
     if (C->rows != p->A.rows || C->cols != p->B.cols) return SPG_STATUS_INVALID_VALUE;
     if (C->value_type != p->A.value_type) return SPG_STATUS_INVALID_VALUE;
     if (C->indptr != p->c_indptr || C->indptr_type != p->c_indptr_type) return SPG_STATUS_INVALID_VALUE;
@@ -1764,8 +1800,10 @@ spg_status_t spg_numeric_tiles(spg_handle_t h, spg_plan_t p, const void* alpha, 
         using T = decltype(tag);
         T a;
         std::memcpy(&a, alpha, sizeof(T));
-        return i64 ? tile_numeric<T, int64_t>(h, *p, (int32_t*)C->indices, (T*)C->values, a, g0, g1, (const T*)tm)
-                   : tile_numeric<T, int32_t>(h, *p, (int32_t*)C->indices, (T*)C->values, a, g0, g1, (const T*)tm);
+        // value tiles [g0, g1) = numeric tiles [g0 * RG, min(G, g1 * RG))
+        const int64_t t0 = g0 << p->rgs, t1 = std::min<int64_t>(p->G, g1 << p->rgs);
+        return i64 ? tile_numeric<T, int64_t>(h, *p, (int32_t*)C->indices, (T*)C->values, a, t0, t1, (const T*)tm)
+                   : tile_numeric<T, int32_t>(h, *p, (int32_t*)C->indices, (T*)C->values, a, t0, t1, (const T*)tm);
     });
 }
 
@@ -1841,6 +1879,7 @@ spg_status_t spg_plan_info(spg_plan_t p, spg_plan_info_t* info, int64_t* chunk_r
     info->path = p->use_tile ? 2 : (p->use_short ? 1 : 0);
     info->tile_width = p->use_tile ? (1 << p->tws) : 0;
     info->tiles_per_row = p->use_tile ? p->G : 0;
+    info->record_group = p->use_tile ? (1 << p->rgs) : 0;
     info->dense_tiles = tile_dense(*p) ? 1 : 0;
     const bool chunked = p->alg == SPG_ALG3 && p->chunk_rows.size() > 1;
     info->n_chunks = chunked ? (int64_t)p->chunk_rows.size() - 1 : 1;

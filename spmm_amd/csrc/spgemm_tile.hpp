@@ -211,30 +211,42 @@ __device__ __forceinline__ int sentinel_col(int i) {
 __host__ __device__ constexpr int sentinel_region(int dense_tw) { return dense_tw == 1024 ? 0 : dense_tw == 2048 ? 1 : 2; }
 
 // ---------------------------------------------------------------------------------------
-// Tile-major B.  For every numeric tile g, B's entries with columns in g, row by row: a CSR
-// of B's column slice g, the slices one after another.  tptr[g*(K+1) + k] is the offset of
-// row k's segment of tile g in the record array and tptr[g*(K+1) + K] the start of tile g+1,
-// so a (row, tile) item finds each A entry's segment with two adjacent 4-byte loads from a
-// K-entry table, and the items of one tile read one contiguous slice of B (an XCD working
-// through a tile keeps that slice and its table in its L2).  Built once per plan from the
-// row-major boundary index (k_tile_index, a temporary):
-//   k_bt_count   segment lengths into tptr (tile-major) and symbolic-tile starts into sidx
+// Tile-major B in record groups.  Tiles are taken RG = 1 << rgs at a time (a record group:
+// RG adjacent column tiles); for every group, B's entries with columns in the group, row by
+// row, and inside a row tile by tile -- i.e. the tile-major layout of tiles RG times as wide,
+// whose every row segment is cut at the RG - 1 inner tile boundaries.  The group's segment
+// table has K*RG + 1 words: word k*RG + t is the offset of row k's segment of tile t of the
+// group, and its successor (word k*RG + t + 1) is that segment's end -- the next tile's start
+// in the same row, or the next row's first segment; word K*RG is the group's end.  With
+// RG = 1 this is the plain tile-major layout: tile g's table at g*(K+1), one word per row.
+// A (row, tile) item finds each A entry's segment with two adjacent 4-byte loads; the RG
+// tiles of one row read ONE contiguous run of records per B row (k_tile_sp's cooperative
+// blocks walk it with one wave per tile, so a cache line carries the segments of several
+// tiles instead of one).  Built once per plan from the row-major boundary index (k_tile_index
+// over the group-padded tile count, a temporary):
+//   k_bt_count   segment lengths into tptr and symbolic-tile starts into sidx
 //   k_scan_lb    lengths -> offsets, in place
 //   k_bt_pack    every B entry to its place (column, value record)
-__global__ __launch_bounds__(256) void k_bt_count(int64_t K, int G, int R, const uint2* __restrict__ tidx,
-                                                  int32_t* __restrict__ tptr, uint32_t* __restrict__ sidx) {
-    const int64_t n = K * G;
+// Segment table of tile g (its words at stride RG from there).
+__host__ __device__ __forceinline__ int64_t tile_table_off(int g, int64_t K, int rgs) {
+    return (int64_t)(g >> rgs) * ((K << rgs) + 1) + (g & ((1 << rgs) - 1));
+}
+// Gp = the group-padded tile count (a multiple of RG); tiles g >= G (padding) get no entries.
+__global__ __launch_bounds__(256) void k_bt_count(int64_t K, int Gp, int G, int R, const uint2* __restrict__ tidx,
+                                                  int32_t* __restrict__ tptr, uint32_t* __restrict__ sidx, int rgs) {
+    const int64_t n = K * Gp;
     const int Gs = (G + R - 1) / R;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n + G; i += (int64_t)gridDim.x * 256) {
-        if (i >= n) {   // the end slot of each tile
-            tptr[(i - n) * (K + 1) + K] = 0;
+    const int Gq = Gp >> rgs;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n + Gq; i += (int64_t)gridDim.x * 256) {
+        if (i >= n) {   // the end slot of each group
+            tptr[(i - n) * ((K << rgs) + 1) + (K << rgs)] = 0;
             continue;
         }
-        const int64_t k = i / G;
-        const int g = (int)(i - k * G);
+        const int64_t k = i / Gp;
+        const int g = (int)(i - k * Gp);
         const uint2 se = tidx[i];
-        tptr[(int64_t)g * (K + 1) + k] = (int32_t)(se.y - se.x);
-        if (g % R == 0) sidx[k * (Gs + 1) + g / R] = se.x;
+        tptr[tile_table_off(g, K, rgs) + (k << rgs)] = (int32_t)(se.y - se.x);
+        if (g < G && g % R == 0) sidx[k * (Gs + 1) + g / R] = se.x;
         if (g == G - 1) sidx[k * (Gs + 1) + Gs] = se.y;
     }
 }
@@ -249,7 +261,7 @@ template <typename T, typename IP, int MODE = 0>
 __global__ __launch_bounds__(256) void k_bt_pack(int64_t K, const IP* __restrict__ Bp, const int32_t* __restrict__ Bj,
                                                  const T* __restrict__ Bx, int tws,
                                                  const int32_t* __restrict__ tptr, uint32_t* __restrict__ rec,
-                                                 int64_t nnzB, T* __restrict__ tm = nullptr) {
+                                                 int64_t nnzB, T* __restrict__ tm, int rgs) {
     const int l = lane_id();
     if (MODE != 2)
         for (int i = blockIdx.x * 256 + threadIdx.x; i < SENT_REGIONS * SENT_N; i += gridDim.x * 256)
@@ -269,7 +281,7 @@ __global__ __launch_bounds__(256) void k_bt_pack(int64_t K, const IP* __restrict
         const int s0 = max(wave_incl_max_dpp((in && g != gp) ? e : -1), carry);
         carry = readlane_i(s0, WAVE - 1);
         if (in) {
-            const int64_t at = (int64_t)tptr[(int64_t)g * (K + 1) + k] + (e - s0);
+            const int64_t at = (int64_t)tptr[tile_table_off(g, K, rgs) + (k << rgs)] + (e - s0);
             if constexpr (MODE == 0) store_rec(rec, at, c & ((1 << tws) - 1), Bx[r0 + e]);
             else if constexpr (MODE == 1) store_rec_col<T>(rec, at, c & ((1 << tws) - 1));
             else tm[at] = Bx[r0 + e];
@@ -287,11 +299,11 @@ __global__ __launch_bounds__(256) void k_bt_fill(const int32_t* __restrict__ lo,
         store_rec_val<T>(rec, r, tm[r]);
 }
 
-// (start, end) of B row k's segment in a tile: two adjacent table words with one 8-byte
-// load (4-byte aligned: one request instead of two)
-__device__ __forceinline__ uint2 seg_pair(const int32_t* __restrict__ tp, int32_t k) {
+// (start, end) of B row k's segment in a tile (tp = tptr + tile_table_off(g, ..)): two
+// adjacent table words with one 8-byte load (4-byte aligned: one request instead of two)
+__device__ __forceinline__ uint2 seg_pair(const int32_t* __restrict__ tp, int32_t k, int rgs) {
     uint2 v;
-    __builtin_memcpy(&v, tp + k, sizeof(v));
+    __builtin_memcpy(&v, tp + ((int64_t)k << rgs), sizeof(v));
     return v;
 }
 
@@ -628,7 +640,7 @@ __global__ __launch_bounds__(tile_num_wpb<DENSE>() * WAVE) void k_tile(
     const int32_t* __restrict__ Aj, const T* __restrict__ Ax, int64_t K,
     const uint32_t* __restrict__ brec, const int32_t* __restrict__ tptr,
     const uint32_t* __restrict__ bitmap, const int64_t* __restrict__ item_off,
-    int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha, uint32_t it_lo, uint32_t it_hi) {
+    int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha, uint32_t it_lo, uint32_t it_hi, int rgs) {
     constexpr int diag = SPG_TILE_DIAG;   // 0 in every shipped build (timing-only diagnostics)
     constexpr int U = sizeof(T) > 8 ? 4 : 8;   // chunks in flight (complex128: half)
     static_assert(U % RU == 0, "round groups split the chunks in flight");
@@ -645,7 +657,7 @@ __global__ __launch_bounds__(tile_num_wpb<DENSE>() * WAVE) void k_tile(
         const int g = (int)(it / (uint32_t)nrows);
         const int64_t row = row0 + (int64_t)(it - (uint32_t)g * (uint32_t)nrows);
         const int64_t item = (row - row0) * G + g;   // items (and bitmaps) of this chunk of rows
-        const int32_t* __restrict__ tp = tptr + (int64_t)g * (K + 1);   // tile g's segment table
+        const int32_t* __restrict__ tp = tptr + tile_table_off(g, K, rgs);   // tile g's segment table
         const int lo = g * TW;
         const int64_t a0 = Ap[row];
         const int nA = (int)(Ap[row + 1] - a0);
@@ -704,7 +716,7 @@ __global__ __launch_bounds__(tile_num_wpb<DENSE>() * WAVE) void k_tile(
 #pragma unroll
         for (int q = 0; q < NB; ++q) {
             sq[q] = make_uint2(0u, 0u);
-            if (kq[q] >= 0) sq[q] = seg_pair(tp, kq[q]);
+            if (kq[q] >= 0) sq[q] = seg_pair(tp, kq[q], rgs);
         }
         // lane info of one batch of A entries: (first B index, count) of its tile segment
         auto batch = [&](int b, int& cnt, int& off, int& Pb, T& bav) {
@@ -720,7 +732,7 @@ __global__ __launch_bounds__(tile_num_wpb<DENSE>() * WAVE) void k_tile(
                         av = aq[q];
                     }
             } else if (b + l < nA) {
-                const uint2 se = seg_pair(tp, Aj[a0 + b + l]);
+                const uint2 se = seg_pair(tp, Aj[a0 + b + l], rgs);
                 cnt = (int)(se.y - se.x);
                 beg = (IP)se.x;
                 av = Ax[a0 + b + l];

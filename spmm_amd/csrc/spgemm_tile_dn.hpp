@@ -180,7 +180,7 @@ template <typename T, int NB, int MKB, typename L, typename Slot, typename Hit>
 __device__ __forceinline__ void dn_walk(L* lp, T* acc, int l, const int32_t* __restrict__ tp, int64_t a0, int nA,
                                         T (&aq)[NB], uint2 (&sq)[NB], const int32_t* __restrict__ Aj,
                                         const T* __restrict__ Ax, const char* __restrict__ rb, uint32_t sent,
-                                        Slot&& slot, Hit&& hit) {
+                                        int rgs, Slot&& slot, Hit&& hit) {
     constexpr int U = (sizeof(T) > 8 ? 4 : 8) * (MKB / 8);   // chunks in flight
     constexpr int DN_MK = MKB * WAVE;                         // products per marker group
     constexpr uint32_t RB = (uint32_t)rec_bytes<T>();   // bytes of one B record
@@ -202,7 +202,7 @@ __device__ __forceinline__ void dn_walk(L* lp, T* acc, int l, const int32_t* __r
                 aq[q] = aq[q + 1];
             }
         } else if (b + l < nA) {
-            const uint2 se = seg_pair(tp, Aj[a0 + b + l]);
+            const uint2 se = seg_pair(tp, Aj[a0 + b + l], rgs);
             cnt = (int)(se.y - se.x);
             bb = se.x * RB;
             av = Ax[a0 + b + l];
@@ -300,7 +300,7 @@ template <typename T, int TWD>
 __device__ __forceinline__ void dn_emit(DnLds<T, TWD>& S, int l, int TW, int lo, int nnz, const int32_t* __restrict__ tp,
                                         int64_t a0, int nA, const int32_t* __restrict__ Aj,
                                         const char* __restrict__ rb, int32_t* __restrict__ crow,
-                                        T* __restrict__ xrow, T alpha) {
+                                        T* __restrict__ xrow, T alpha, int rgs) {
     constexpr uint32_t RB = (uint32_t)rec_bytes<T>();
     wsync();
     // the item's structure, 64 columns at a time: hit[] or (dn_sent) the non -0.0 slots
@@ -339,7 +339,7 @@ __device__ __forceinline__ void dn_emit(DnLds<T, TWD>& S, int l, int TW, int lo,
             // reached -0.0 slot into +0.0, then write the item again.
             for (int b = 0; b < nA; b += WAVE) {
                 if (b + l < nA) {
-                    const uint2 se = seg_pair(tp, Aj[a0 + b + l]);
+                    const uint2 se = seg_pair(tp, Aj[a0 + b + l], rgs);
                     for (uint32_t i = se.x; i < se.y; ++i) {
                         int c;
                         T v;
@@ -379,13 +379,13 @@ __device__ __forceinline__ void dn_item(DnLds<T, TWD>& S, int l, int TW, int lo,
                                         const int32_t* __restrict__ Aj,
                                         const T* __restrict__ Ax, const char* __restrict__ rb, uint32_t sent,
                                         int32_t* __restrict__ crow,
-                                        T* __restrict__ xrow, T alpha) {
+                                        T* __restrict__ xrow, T alpha, int rgs) {
     dn_clear(S, l, TW);
-    dn_walk<T, NB, dn_mkb(TWD)>(&S, S.acc, l, tp, a0, nA, aq, sq, Aj, Ax, rb, sent, [&](int c) { return c; },
+    dn_walk<T, NB, dn_mkb(TWD)>(&S, S.acc, l, tp, a0, nA, aq, sq, Aj, Ax, rb, sent, rgs, [&](int c) { return c; },
                    [&](int c) {
                        if constexpr (!dn_sent<T>()) S.hit[c] = 1;
                    });
-    dn_emit<T, TWD>(S, l, TW, lo, nnz, tp, a0, nA, Aj, rb, crow, xrow, alpha);
+    dn_emit<T, TWD>(S, l, TW, lo, nnz, tp, a0, nA, Aj, rb, crow, xrow, alpha, rgs);
 }
 // Numeric pass on dense tiles: one wave per (row, tile) item, items tile-major over the
 // XCD-aware block map (an XCD works through one tile at a time, so the tile's B slice and
@@ -397,7 +397,7 @@ __global__ __launch_bounds__(DN_WPB * WAVE) void k_tile_dn(
     const int32_t* __restrict__ Aj, const T* __restrict__ Ax, int64_t K,
     const uint32_t* __restrict__ brec, const int32_t* __restrict__ tptr,
     const int64_t* __restrict__ item_off, int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha, uint32_t sent,
-    uint32_t it_lo, uint32_t it_hi) {
+    uint32_t it_lo, uint32_t it_hi, int rgs) {
     static_assert(OrderedLdsAdd<T>::value, "ordered LDS add needed");
     constexpr int NB = sizeof(T) > 8 ? 4 : 8;    // A batches preloaded per item
     __shared__ __attribute__((aligned(16))) DnLds<T, TWD> lds[DN_WPB];
@@ -414,7 +414,7 @@ __global__ __launch_bounds__(DN_WPB * WAVE) void k_tile_dn(
         const int64_t obase = ld_a(item_off + item);
         const int nnz = (int)(ld_a(item_off + item + 1) - obase);
         if (nnz == 0) continue;                      // (no product reaches this tile)
-        const int32_t* __restrict__ tp = tptr + (int64_t)g * (K + 1);
+        const int32_t* __restrict__ tp = tptr + tile_table_off(g, K, rgs);
         const int64_t a0 = Ap[row];
         const int nA = (int)(Ap[row + 1] - a0);
         int32_t kq[NB];
@@ -430,8 +430,9 @@ __global__ __launch_bounds__(DN_WPB * WAVE) void k_tile_dn(
             }
         }
 #pragma unroll
-        for (int q = 0; q < NB; ++q) sq[q] = kq[q] >= 0 ? seg_pair(tp, kq[q]) : make_uint2(0u, 0u);
-        dn_item<T, NB, TWD>(S, l, TW, g * TW, nnz, tp, a0, nA, aq, sq, Aj, Ax, rb, sent, Cj + obase, Cx + obase, alpha);
+        for (int q = 0; q < NB; ++q) sq[q] = kq[q] >= 0 ? seg_pair(tp, kq[q], rgs) : make_uint2(0u, 0u);
+        dn_item<T, NB, TWD>(S, l, TW, g * TW, nnz, tp, a0, nA, aq, sq, Aj, Ax, rb, sent, Cj + obase, Cx + obase, alpha,
+                            rgs);
     }
 }
 
@@ -448,47 +449,71 @@ __global__ __launch_bounds__(DN_WPB * WAVE) void k_tile_dn(
 // bitmap words) and, fp64 only, 8192 columns (2048-slot windows, 256 words: config 5's
 // shape, numeric 128.7 -> 103.9 ms; 16384 columns measured 143 ms with 2048-slot windows and,
 // round 4, 138 ms with one 4096-slot window: 39 KB of LDS per wave leaves 4 waves per CU).
-template <int CAP> struct SpGeom {
-    static constexpr int NWMAX = CAP / 8;          // bitmap words of the widest tile (TW = 4 * CAP)
-    static constexpr int WPL = NWMAX / WAVE;       // bitmap words per lane (at most)
+// LDS geometry of a sparse-tile kernel: CAP window slots, NW bitmap words (TW <= 32 * NW
+// columns), DUMMY lane slots past the window (the out-of-window and sentinel products add
+// there: lane l into CAP + (l % DUMMY)), MKB chunks per marker group.
+template <int CAP_, int NW_, int DUMMY_, int MKB_> struct SpCfg {
+    static constexpr int CAP = CAP_, NW = NW_, DUMMY = DUMMY_, MKB = MKB_;
+    static constexpr int WPL = NW / WAVE;          // bitmap words per lane (at most)
 };
-template <typename T, int CAP> struct SpLds {
-    T acc[CAP + WAVE];            // compact accumulator of one window; + lane-private slots
-    uint2 bw[SpGeom<CAP>::NWMAX];   // (bitmap word, popcount prefix)
+using SpCfg1024 = SpCfg<1024, 128, WAVE, 8>;    // tiles of <= 4096 columns (11.3 KB per wave)
+using SpCfg2048 = SpCfg<2048, 256, WAVE, 16>;   // fp64 8192-column tiles (21.0 KB)
+// fp64 8192-column tiles in cooperative blocks of 4 waves (k_tile_sp<.., RG = 4>): 20,432 bytes per
+// wave, so two 4-wave blocks (8 waves) fit a CU's 160 KB; 2032 slots per window (config 5's
+// items hold 1887 +- 40 entries) and 8 lane slots (an out-of-window add conflicts at most 8 ways)
+using SpCfgRG = SpCfg<2032, 256, 8, 16>;
+template <typename T, typename CF> struct SpLds {
+    T acc[CF::CAP + CF::DUMMY];         // compact accumulator of one window; + lane slots
+    uint2 bw[CF::NW];                   // (bitmap word, popcount prefix)
     DnEnt<T> ent[WAVE + 1];
-    uint8_t mk[dn_mkb(CAP) * WAVE];
+    uint8_t mk[CF::MKB * WAVE];
 #ifdef SPG_LDS_PAD
     uint8_t pad[SPG_LDS_PAD];   // (A/B builds: occupancy sensitivity)
 #endif
 };
-constexpr int SP_WPB = 1;   // 11.3 KB of LDS per wave: one-wave blocks pack a CU best
 
-template <typename T, typename IP, int SP_CAP>
-__global__ __launch_bounds__(SP_WPB * WAVE) __attribute__((amdgpu_waves_per_eu((sizeof(T) > 8 || SP_CAP > 1024) ? 2 : 4)))
+// RG = 1: one-wave blocks, items tile-major (item it = (tile, row)).
+// RG > 1 (cooperative record groups, round 5): blocks of RG waves, items group-major (it =
+// (group, row)); wave t of the block takes tile group*RG + t of the same row.  The RG tiles'
+// segments of one B row are adjacent in the record-group layout (k_bt_pack), so the block's
+// waves walk one contiguous run of records per A entry instead of RG separate ~80-byte
+// segments in RG slices: config 5's segments are 8 records (82 bytes) per 8192-column tile,
+// and a lone segment costs 1.6 128-byte lines.  A barrier at every item keeps the waves on
+// the same A entries, so the lines they share are fetched once.  The accumulation is per
+// wave and per tile, exactly as with RG = 1 (same results bit for bit).
+template <typename T, typename IP, typename CF, int RG>
+__global__ __launch_bounds__(RG * WAVE) __attribute__((amdgpu_waves_per_eu((sizeof(T) > 8 || CF::CAP > 1024) ? 2 : 4)))
 void k_tile_sp(
     int64_t row0, int64_t nrows, int tws, int G, const IP* __restrict__ Ap,
     const int32_t* __restrict__ Aj, const T* __restrict__ Ax, int64_t K,
     const uint32_t* __restrict__ brec, const int32_t* __restrict__ tptr, const uint32_t* __restrict__ bitmap,
     const int64_t* __restrict__ item_off, int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha, uint32_t sent,
-    uint32_t it_lo, uint32_t it_hi) {
+    uint32_t it_lo, uint32_t it_hi, int rgs) {
     static_assert(OrderedLdsAdd<T>::value, "ordered LDS add needed");
-    static_assert(sizeof(T) * (SP_CAP + WAVE) >= 4 * SP_CAP, "column list fits the accumulator");
-    constexpr int SP_WPL = SpGeom<SP_CAP>::WPL;
+    constexpr int SP_CAP = CF::CAP;
+    constexpr int SP_DUMMY = CF::DUMMY;
+    static_assert((SP_DUMMY & (SP_DUMMY - 1)) == 0, "lane slots: a power of two");
+    static_assert(sizeof(T) * (SP_CAP + SP_DUMMY) >= 4 * SP_CAP, "column list fits the accumulator");
+    constexpr int SP_WPL = CF::WPL;
     constexpr int NB = sizeof(T) > 8 ? 4 : 8;
-    __shared__ __attribute__((aligned(16))) SpLds<T, SP_CAP> lds[SP_WPB];
+    __shared__ __attribute__((aligned(16))) SpLds<T, CF> lds[RG];
     const int l = lane_id();
     const int wv = uniform((int)(threadIdx.x >> 6));
-    SpLds<T, SP_CAP>& S = lds[wv];
+    SpLds<T, CF>& S = lds[wv];
     const int TW = 1 << tws;
     const int nw = TW >> 5;                    // bitmap words of a tile
     const int wpl = (nw + WAVE - 1) / WAVE;    // words per lane (<= SP_WPL)
     const char* __restrict__ rb = reinterpret_cast<const char*>(brec);
     const bool one = alpha == (T)1;
-    for (uint32_t it = it_lo + xcd_block(gridDim.x) * SP_WPB + wv; it < it_hi; it += gridDim.x * SP_WPB) {
-        const int g = (int)(it / (uint32_t)nrows);
-        const int64_t row = row0 + (int64_t)(it - (uint32_t)g * (uint32_t)nrows);
+    // one item per block and sweep (RG == 1: a one-wave block's; RG > 1: the group's RG tiles of a row)
+    for (uint32_t it = it_lo + xcd_block(gridDim.x); it < it_hi; it += gridDim.x) {
+        if constexpr (RG > 1) __syncthreads();    // the block's waves start every item together
+        const int grp = (int)(it / (uint32_t)nrows);
+        const int64_t row = row0 + (int64_t)(it - (uint32_t)grp * (uint32_t)nrows);
+        const int g = RG == 1 ? grp : grp * RG + wv;
+        if (RG > 1 && g >= G) continue;           // (a padding tile of the last group)
         const int64_t item = (row - row0) * G + g;
-        const int32_t* __restrict__ tp = tptr + (int64_t)g * (K + 1);
+        const int32_t* __restrict__ tp = tptr + tile_table_off(g, K, rgs);
         const int64_t a0 = Ap[row];
         const int nA = (int)(Ap[row + 1] - a0);
         if (nA <= 0) continue;
@@ -534,7 +559,7 @@ void k_tile_sp(
                 }
             }
 #pragma unroll
-            for (int q = 0; q < NB; ++q) sq[q] = kq[q] >= 0 ? seg_pair(tp, kq[q]) : make_uint2(0u, 0u);
+            for (int q = 0; q < NB; ++q) sq[q] = kq[q] >= 0 ? seg_pair(tp, kq[q], rgs) : make_uint2(0u, 0u);
         };
         preload();
         const int64_t obase = item_off[item];
@@ -562,9 +587,9 @@ void k_tile_sp(
             wsync();
             for (int p = l; p < wn; p += WAVE) S.acc[p] = (T)0;
             if (L0 > 0) preload();   // (the walk consumes the queue; rare later windows reload it)
-            dn_walk<T, NB, dn_mkb(SP_CAP)>(&S, S.acc, l, tp, a0, nA, aq, sq, Aj, Ax, rb, sent,
+            dn_walk<T, NB, CF::MKB>(&S, S.acc, l, tp, a0, nA, aq, sq, Aj, Ax, rb, sent, rgs,
                            [&](int rc) -> int {
-                               if (rc < clo || rc >= chi) return SP_CAP + l;   // (sentinels too)
+                               if (rc < clo || rc >= chi) return SP_CAP + (l & (SP_DUMMY - 1));   // (sentinels too)
                                const uint2 b = S.bw[rc >> 5];
                                return (int)b.y + __popc(b.x & ((1u << (rc & 31)) - 1u)) - wb;
                            },
@@ -577,7 +602,7 @@ void k_tile_sp(
                     for (int p0 = 0; p0 < wn; p0 += 4 * WAVE) {
                         T v[4];
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) v[e] = S.acc[min(p0 + e * WAVE + l, SP_CAP + WAVE - 1)];
+                        for (int e = 0; e < 4; ++e) v[e] = S.acc[min(p0 + e * WAVE + l, SP_CAP + SP_DUMMY - 1)];
 #pragma unroll
                         for (int e = 0; e < 4; ++e) {
                             const int p = p0 + e * WAVE + l;

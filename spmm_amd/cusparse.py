@@ -256,7 +256,9 @@ def _numeric_by_tiles(h, plan, b, al, vc, by_tiles) -> bool:
     # (a development library built without the tile-group entry points: spg_numeric)
     has_tiles = all(hasattr(lib, f) for f in ("spg_tile_value_offsets", "spg_tile_values", "spg_numeric_tiles"))
     if has_tiles and info.path == 2 and info.n_chunks == 1:
-        G = int(info.tiles_per_row)
+        # value tiles: record_group adjacent numeric tiles (include/spgemm.h)
+        rg = max(1, int(info.record_group))
+        G = (int(info.tiles_per_row) + rg - 1) // rg
         offs = (ctypes.c_int64 * (G + 1))()
         st = lib.spg_tile_value_offsets(h.ptr, plan, offs, G + 1)
         if st == 0:
@@ -264,7 +266,7 @@ def _numeric_by_tiles(h, plan, b, al, vc, by_tiles) -> bool:
                 tm = torch.empty(max(b.nnz, 1), dtype=b.data.dtype, device=b.data.device)
                 check(lib.spg_tile_values(h.ptr, plan, ctypes.c_void_p(tm.data_ptr())), "spg_tile_values")
                 return tm[:b.nnz]
-            geom = {"tile_width": int(info.tile_width), "tiles": G, "offsets": np.frombuffer(offs, dtype=np.int64).copy(),
+            geom = {"tile_width": int(info.tile_width) * rg, "tiles": G, "offsets": np.frombuffer(offs, dtype=np.int64).copy(),
                     "tile_values": tile_values, "dtype": b.data.dtype}
         elif st != _lib.STATUS_NOT_SUPPORTED:
             check(st, "spg_tile_value_offsets")
@@ -382,7 +384,7 @@ def plan_info(a: csr_matrix, b: csr_matrix, alg: int = 0, chunk_fraction: float 
         check(h.lib.spg_plan_info(plan, ctypes.byref(info), rows, info.n_chunks + 1), "spg_plan_info")
         return {"path": ("general", "short", "tile")[info.path], "tile_width": info.tile_width,
                 "tiles_per_row": info.tiles_per_row, "dense_tiles": bool(info.dense_tiles),
-                "lds_ordered": bool(info.lds_ordered),
+                "lds_ordered": bool(info.lds_ordered), "record_group": int(info.record_group),
                 "chunk_rows": [int(x) for x in rows]}
     finally:
         h.lib.spg_plan_destroy(plan)

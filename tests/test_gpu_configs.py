@@ -65,7 +65,7 @@ def _expected_nnz(a_lens, n, density):
 
 
 @torch.no_grad()
-def _check_structure(A, B, C, n, density, tile_width):
+def _check_structure(A, B, C, n, density, tile_width, record_group=1):
     """Size-independent properties of C over every row (device-side, in row chunks).
     Returns (P, per-row nnz(C) on the host, rows with a tile item over TILE_CAP entries)."""
     m = A.shape[0]
@@ -102,7 +102,7 @@ def _check_structure(A, B, C, n, density, tile_width):
         assert bool(ok.all()), f"columns not increasing in rows [{r0}, {r1})"
         rid = torch.repeat_interleave(torch.arange(r1 - r0, device=cols.device), lens[r0:r1])
         items = torch.bincount(rid * G + (cols // tile_width).to(torch.int64), minlength=(r1 - r0) * G)
-        big = torch.nonzero(items.view(r1 - r0, G).max(dim=1).values > window_cap(tile_width)).flatten() + r0
+        big = torch.nonzero(items.view(r1 - r0, G).max(dim=1).values > window_cap(tile_width, record_group)).flatten() + r0
         over_cap.append(big.cpu().numpy())
         del cols, start, ok, rid, items
     return int(P_i.sum()), lens.cpu().numpy(), np.concatenate(over_cap) if over_cap else np.zeros(0, np.int64)
@@ -111,10 +111,13 @@ def _check_structure(A, B, C, n, density, tile_width):
 TILE_CAP = 1024   # entries of one tile-item accumulator window (spgemm_tile.hpp)
 
 
-def window_cap(tile_width):
-    """Accumulator window of a sparse tile item: 2048 slots on 8192-column tiles
-    (k_tile_sp<double, .., 2048>), else TILE_CAP."""
-    return 2048 if tile_width == 8192 else TILE_CAP
+def window_cap(tile_width, record_group=1):
+    """Accumulator window of a sparse tile item: on 8192-column tiles 2048 slots
+    (k_tile_sp<double, .., SpCfg2048, 1>) or, in cooperative record groups, 2032
+    (SpCfgRG: two 4-wave blocks per CU); else TILE_CAP."""
+    if tile_width == 8192:
+        return 2032 if record_group > 1 else 2048
+    return TILE_CAP
 
 
 def _stratified_rows(A, C_lens, chunk_rows, over_cap, total=2048, seed=0):
@@ -185,7 +188,8 @@ def test_large_config_stratified_and_properties(n, density, alg, cf, expect_prod
     assert len(info["chunk_rows"]) - 1 >= chunks if chunks > 1 else len(info["chunk_rows"]) == 2, info
     C = cusparse.spgemm(A, B, alg=alg, chunk_fraction=cf)
     torch.cuda.synchronize()
-    P, C_lens, over_cap = _check_structure(A, B, C, n, density, info["tile_width"])
+    P, C_lens, over_cap = _check_structure(A, B, C, n, density, info["tile_width"],
+                                          info.get("record_group", 1))
     assert P == cusparse.num_products(A, B)
     assert abs(P - expect_products) / expect_products < 0.02
     rows = _stratified_rows(A, C_lens, info["chunk_rows"], over_cap)

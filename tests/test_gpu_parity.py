@@ -6,6 +6,7 @@ exactly scipy's rule (the fp tolerance of the north star, |c - c_ref| <= gamma_m
 is therefore met with margin 0).  Structural zeros are kept (cuSPARSE semantics); after
 eliminate_zeros() the result must equal scipy's, array for array.
 """
+import os
 import numpy as np
 import pytest
 import scipy.sparse as sp
@@ -344,10 +345,21 @@ def test_tile_path_sparse_8192():
     dA, dB = csr_matrix(A, device=_dev()), csr_matrix(B, device=_dev())
     info = cusparse.plan_info(dA, dB, alg=2)
     assert info["tile_width"] == 8192 and not info["dense_tiles"], info
+    # cooperative record groups of 4 tiles (k_tile_sp<.., SpCfgRG, 4>): G = 5 tiles, so the
+    # second group holds one real tile and three padding tiles
+    assert info["record_group"] == 4 and info["tiles_per_row"] == 5, info
     ref = oracle.spgemm(A, B, alpha=0.5, keep_zeros=True, sort=True)
     assert np.diff(ref[0]).max() > 2 * 2048 * 4   # dense rows: several windows per item
     for alg, cf in [(1, 0.2), (2, 0.2), (3, 0.2), ("3c", 0.02)]:
         _assert_same(_gpu(A, B, alg=alg, alpha=0.5, cf=cf), ref)
+    # the one-wave kernel over plain tile-major records (SPG_SP_RECORD_GROUP=1): same bits
+    os.environ["SPG_SP_RECORD_GROUP"] = "1"
+    try:
+        assert cusparse.plan_info(dA, dB, alg=2)["record_group"] == 1
+        for alg, cf in [(2, 0.2), ("3c", 0.02)]:
+            _assert_same(_gpu(A, B, alg=alg, alpha=0.5, cf=cf), ref)
+    finally:
+        del os.environ["SPG_SP_RECORD_GROUP"]
 
 
 def test_tile_path_dense_tiles_fp32_int64():
