@@ -264,6 +264,12 @@ inline unsigned tile_grid(int64_t tasks, int wpb = TILE_WPB) {
     const int64_t nb = std::max<int64_t>(1, std::min<int64_t>(grid_for(tasks, wpb), cap));
     return (unsigned)((nb + 7) / 8 * 8);
 }
+// grid of a cooperative tile kernel: one task per block of `wpb` waves (same caps)
+inline unsigned coop_grid(int64_t tasks, int wpb) {
+    const int64_t cap = ((int64_t)1 << 31) / ((int64_t)wpb * WAVE);
+    const int64_t nb = std::max<int64_t>(1, std::min<int64_t>(tasks, cap));
+    return (unsigned)((nb + 7) / 8 * 8);
+}
 
 // symbolic tile: the narrowest width >= the numeric tile whose B segments (expected B row
 // entries per tile) reach 64 entries -- long coalesced reads -- capped at 65536 columns
@@ -592,6 +598,17 @@ inline int64_t rec_groups(const spg_plan_s& p) { return ((int64_t)p.G + (1 << p.
 inline int64_t tiles_padded(const spg_plan_s& p) { return rec_groups(p) << p.rgs; }
 inline int64_t group_words(const spg_plan_s& p) { return (p.B.rows << p.rgs) + 1; }   // one group's table
 inline int64_t bt_entries(const spg_plan_s& p) { return p.use_tile ? rec_groups(p) * group_words(p) : 0; }
+// k_tile_sym8 in cooperative blocks of SPG_SYM_CO waves (one row's adjacent symbolic tiles)
+// when a row has at least that many symbolic tiles (config 5: 4 of 65536 columns);
+// SPG_SYM_COOP=0 (read per call: a schedule-only switch for A/B timing and the tests) keeps
+// the two-wave blocks of one task per wave
+#ifndef SPG_SYM_CO
+#define SPG_SYM_CO 4
+#endif
+inline bool sym_co_off() {
+    const char* e = std::getenv("SPG_SYM_COOP");
+    return e && std::strcmp(e, "0") == 0;
+}
 // fp64 8192-column sparse tiles (config 5's shape) run in cooperative record groups of
 // 1 << SPG_SP_RGS tiles (k_tile_sp<.., RG>); every other tile plan keeps RG = 1
 #ifndef SPG_SP_RGS
@@ -938,8 +955,15 @@ spg_status_t tile_sym_chunk(spg_handle_t h, spg_plan_s& p, int64_t c) {
                          dim3(SEG_WPB * WAVE), r0, n, p.tws, p.G, p.twss, (const IP*)p.A.indptr,
                          (const int32_t*)p.A.indices, (const IP*)p.B.indptr, (const uint16_t*)p.bj16,
                          (const uint32_t*)p.sidx, tile_dense(p) ? (uint32_t*)nullptr : p.bitmap, items);
+        else if (SPG_SYM8 && SPG_SYM_CO > 1 && sym_tiles(p) >= SPG_SYM_CO && !sym_co_off())
+            // cooperative blocks: SPG_SYM_CO symbolic tiles of one row per block
+            timed_launch(h, SPG_PHASE_SYMBOLIC, k_tile_sym8<IP, SPG_SYM_CO>,
+                         dim3(coop_grid(n * ((sym_tiles(p) + SPG_SYM_CO - 1) / SPG_SYM_CO), SPG_SYM_CO)), dim3(SPG_SYM_CO * WAVE),
+                         r0, n, p.tws, p.G, p.twss, (const IP*)p.A.indptr, (const int32_t*)p.A.indices,
+                         (const IP*)p.B.indptr, (const uint16_t*)p.bj16, (const uint32_t*)p.sidx,
+                         tile_dense(p) ? (uint32_t*)nullptr : p.bitmap, items);
         else if (SPG_SYM8)
-            timed_launch(h, SPG_PHASE_SYMBOLIC, k_tile_sym8<IP>, dim3(tile_grid(n * sym_tiles(p))), dim3(TILE_WPB * WAVE),
+            timed_launch(h, SPG_PHASE_SYMBOLIC, k_tile_sym8<IP, 1>, dim3(tile_grid(n * sym_tiles(p))), dim3(TILE_WPB * WAVE),
                          r0, n, p.tws, p.G, p.twss, (const IP*)p.A.indptr, (const int32_t*)p.A.indices,
                          (const IP*)p.B.indptr, (const uint16_t*)p.bj16, (const uint32_t*)p.sidx,
                          tile_dense(p) ? (uint32_t*)nullptr : p.bitmap, items);
@@ -1067,7 +1091,7 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
                         it_hi = (uint32_t)(q1 * n);
                         nit = (q1 - q0) * n;
                     }
-                    hipExtLaunchKernelGGL((k_tile_sp<T, IP, CF, RG>), dim3(tile_grid(nit, 1)), dim3(RG * WAVE),
+                    hipExtLaunchKernelGGL((k_tile_sp<T, IP, CF, RG>), dim3(coop_grid(nit, RG)), dim3(RG * WAVE),
                                           0, h->stream, kt.a, kt.b, 0, r0, n, p.tws, p.G, Ap, Aj, Ax, p.B.rows,
                                           (const uint32_t*)p.brec, (const int32_t*)p.tptr, (const uint32_t*)p.bitmap,
                                           (const int64_t*)tile_chunk_items(p, c), cj, cx, alpha,

@@ -324,6 +324,66 @@ def test_tile_path_dense_2048(neg):
         _assert_same(_gpu(A, B, alg=alg, cf=cf), ref)
 
 
+def test_tile_path_dense_2048_width_band():
+    """fp64 C rows 24-48 % dense over >= 16384 columns reach 2048-column DENSE tiles through
+    the width loop (spgemm.hip want_tile: 2048 columns hold <= 0.95 * 1024 expected entries),
+    not through the >= 50 % rule: a case in that band,
+    C rows ~30 % dense (expected entries per row / columns = 1 - exp(-avgA * avgB / N)), a
+    ragged last tile, every algorithm with ALG3's chunks forced, bit-exact."""
+    from spmm_amd import cusparse
+    from spmm_amd.sparse import csr_matrix
+    rng = np.random.default_rng(38)
+    n = 20000
+    A = sp.random(180, n, density=0.0042, format="csr", random_state=rng)
+    B = sp.random(n, n, density=0.0042, format="csr", random_state=rng)
+    for M in (A, B):
+        M.sort_indices()
+    ref = oracle.spgemm(A, B, keep_zeros=True, sort=True)
+    frac = (np.diff(ref[0]).mean()) / n
+    assert 0.24 < frac < 0.45, frac
+    dA, dB = csr_matrix(A, device=_dev()), csr_matrix(B, device=_dev())
+    info = cusparse.plan_info(dA, dB, alg=2)
+    assert info["tile_width"] == 2048 and info["dense_tiles"] and info["record_group"] == 1, info
+    for alg, cf in [(1, 0.2), (2, 0.2), ("3c", 0.1)]:
+        _assert_same(_gpu(A, B, alg=alg, cf=cf), ref)
+
+
+def _random_rows(rng, rows, cols, per_row):
+    """CSR with ~per_row random entries per row (numpy, no N^2 sampling), canonical."""
+    r = np.repeat(np.arange(rows), per_row)
+    c = rng.integers(0, cols, size=rows * per_row)
+    M = sp.csr_matrix((rng.random(rows * per_row), (r, c)), shape=(rows, cols))
+    M.sum_duplicates()
+    M.sort_indices()
+    return M
+
+
+def test_tile_path_cooperative_groups_with_padding():
+    """Config 5's cooperative kernels on a shape whose group counts do not divide: 300000
+    columns -> 37 numeric tiles of 8192 (record groups of 4: the last holds 1 real tile and 3
+    padding tiles) and 5 symbolic tiles of 65536 (k_tile_sym8 blocks of 4: the second block
+    has 1 real symbolic tile).  Bit-exact for ALG2 and chunked ALG3, and the same with both
+    cooperative schedules switched off (SPG_SP_RECORD_GROUP=1, SPG_SYM_COOP=0)."""
+    from spmm_amd import cusparse
+    from spmm_amd.sparse import csr_matrix
+    rng = np.random.default_rng(39)
+    n = 300000
+    A = _random_rows(rng, 200, n, 600)
+    B = _random_rows(rng, n, n, 60)
+    dA, dB = csr_matrix(A, device=_dev()), csr_matrix(B, device=_dev())
+    info = cusparse.plan_info(dA, dB, alg=2)
+    assert info["tile_width"] == 8192 and info["tiles_per_row"] == 37 and info["record_group"] == 4, info
+    ref = oracle.spgemm(A, B, alpha=1.5, keep_zeros=True, sort=True, threads=16)
+    for alg, cf in [(2, 0.2), ("3c", 0.1)]:
+        _assert_same(_gpu(A, B, alg=alg, alpha=1.5, cf=cf), ref)
+    os.environ["SPG_SP_RECORD_GROUP"] = "1"
+    os.environ["SPG_SYM_COOP"] = "0"
+    try:
+        _assert_same(_gpu(A, B, alg=2, alpha=1.5), ref)
+    finally:
+        del os.environ["SPG_SP_RECORD_GROUP"], os.environ["SPG_SYM_COOP"]
+
+
 def test_tile_path_sparse_8192():
     """fp64 C rows 10-24 % dense over >= 16384 columns take 8192-column sparse tiles
     (k_tile_sp<double, .., 2048>; config 5's shape): skewed A rows whose items need several
