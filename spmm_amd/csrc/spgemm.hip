@@ -326,34 +326,35 @@ spg_status_t hip_fail(spg_handle_t h, hipError_t e) {
 // k_lds_order_check runs LDSCHK_TRIALS trials of two ds_add_f64 instructions from all 64 lanes
 // into 4 slots with operands whose rounded sums depend on the order; the host replays them in
 // (instruction, lane) order.  Any bit difference sets *ordered = false.
-hipError_t lds_order_check(bool* ordered) {
+template <typename T>
+hipError_t lds_order_check_t(bool* ordered) {
     constexpr int N = LDSCHK_TRIALS * 2 * WAVE;
-    std::vector<double> v(N);
+    std::vector<T> v(N);
     std::vector<int> slot(N);
     uint64_t x = 0x9e3779b97f4a7c15ull;
     auto next = [&] { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return x; };
     for (int i = 0; i < N; ++i) {
         const uint64_t r = next();
         const double m = 1.0 + (double)(r >> 11) * (1.0 / 9007199254740992.0);   // [1, 2)
-        v[i] = std::ldexp((r & 1) ? -m : m, (int)((r >> 1) % 81) - 40);
+        v[i] = (T)std::ldexp((r & 1) ? -m : m, (int)((r >> 1) % 81) - 40);
         slot[i] = (int)((r >> 8) & 3);
     }
-    double *dv = nullptr, *dout = nullptr;
+    T *dv = nullptr, *dout = nullptr;
     int* ds = nullptr;
-    hipError_t e = hipMalloc((void**)&dv, sizeof(double) * N);
+    hipError_t e = hipMalloc((void**)&dv, sizeof(T) * N);
     if (e == hipSuccess) e = hipMalloc((void**)&ds, sizeof(int) * N);
-    if (e == hipSuccess) e = hipMalloc((void**)&dout, sizeof(double) * 4 * LDSCHK_TRIALS);
-    if (e == hipSuccess) e = hipMemcpy(dv, v.data(), sizeof(double) * N, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc((void**)&dout, sizeof(T) * 4 * LDSCHK_TRIALS);
+    if (e == hipSuccess) e = hipMemcpy(dv, v.data(), sizeof(T) * N, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(ds, slot.data(), sizeof(int) * N, hipMemcpyHostToDevice);
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_lds_order_check, dim3(1), dim3(WAVE), 0, 0, (const double*)dv, (const int*)ds, dout);
+        hipLaunchKernelGGL(k_lds_order_check<T>, dim3(1), dim3(WAVE), 0, 0, (const T*)dv, (const int*)ds, dout);
         e = hipGetLastError();
     }
-    std::vector<double> got(4 * LDSCHK_TRIALS);
-    if (e == hipSuccess) e = hipMemcpy(got.data(), dout, sizeof(double) * got.size(), hipMemcpyDeviceToHost);
+    std::vector<T> got(4 * LDSCHK_TRIALS);
+    if (e == hipSuccess) e = hipMemcpy(got.data(), dout, sizeof(T) * got.size(), hipMemcpyDeviceToHost);
     bool ok = e == hipSuccess;
     for (int t = 0; ok && t < LDSCHK_TRIALS; ++t) {
-        double acc[4] = {0.0, 0.0, 0.0, 0.0};
+        T acc[4] = {(T)0, (T)0, (T)0, (T)0};
         for (int i = t * 2 * WAVE; i < (t + 1) * 2 * WAVE; ++i) acc[slot[i]] = acc[slot[i]] + v[i];
         ok = std::memcmp(acc, &got[4 * t], sizeof(acc)) == 0;
     }
@@ -361,6 +362,15 @@ hipError_t lds_order_check(bool* ordered) {
     if (dv) (void)hipFree(dv);
     if (ds) (void)hipFree(ds);
     if (dout) (void)hipFree(dout);
+    return e;
+}
+// both widths: ds_add_f64 (the fp64 / complex128 lean kernels) and ds_add_f32 (the fp32 runs'
+// third-and-later entries, k_tile_dn<float, ..>)
+hipError_t lds_order_check(bool* ordered) {
+    bool o64 = false, o32 = false;
+    hipError_t e = lds_order_check_t<double>(&o64);
+    if (e == hipSuccess) e = lds_order_check_t<float>(&o32);
+    *ordered = o64 && o32;
     return e;
 }
 
@@ -598,21 +608,28 @@ inline int64_t rec_groups(const spg_plan_s& p) { return ((int64_t)p.G + (1 << p.
 inline int64_t tiles_padded(const spg_plan_s& p) { return rec_groups(p) << p.rgs; }
 inline int64_t group_words(const spg_plan_s& p) { return (p.B.rows << p.rgs) + 1; }   // one group's table
 inline int64_t bt_entries(const spg_plan_s& p) { return p.use_tile ? rec_groups(p) * group_words(p) : 0; }
-// k_tile_sym8 in cooperative blocks of SPG_SYM_CO waves (one row's adjacent symbolic tiles)
-// when a row has at least that many symbolic tiles (config 5: 4 of 65536 columns);
-// SPG_SYM_COOP=0 (read per call: a schedule-only switch for A/B timing and the tests) keeps
-// the two-wave blocks of one task per wave
-#ifndef SPG_SYM_CO
-#define SPG_SYM_CO 4
+// fp32 dense tiles take k_tile_dn<float, .., 1024> (plain read-add-write per A entry's run of a
+// chunk) when a tile's expected B segment holds >= SPG_F32_RUN_MIN entries: chunks then hold one
+// or two entries' runs (config 3 at density 0.1: 102-entry segments); shorter segments put many
+// entries in a chunk and keep k_tile's owner rounds.  SPG_F32_RUNS=0 (read per plan: a
+// schedule-only switch for A/B timing and the tests) keeps k_tile.
+#ifndef SPG_F32_RUN_MIN
+#define SPG_F32_RUN_MIN 48
 #endif
-inline bool sym_co_off() {
-    const char* e = std::getenv("SPG_SYM_COOP");
-    return e && std::strcmp(e, "0") == 0;
+inline bool fp32_runs(const spg_plan_s& p) {
+    if (p.A.value_type != SPG_R_32F || p.B.cols <= 0 || p.B.rows <= 0 || (1 << p.tws) > 1024) return false;
+    const char* e = std::getenv("SPG_F32_RUNS");
+    if (e && std::strcmp(e, "0") == 0) return false;
+    const double seg = (double)p.B.nnz / (double)p.B.rows * (double)(1 << p.tws) / (double)p.B.cols;
+    return seg >= SPG_F32_RUN_MIN;
 }
-// fp64 8192-column sparse tiles (config 5's shape) run in cooperative record groups of
-// 1 << SPG_SP_RGS tiles (k_tile_sp<.., RG>); every other tile plan keeps RG = 1
+// fp64 8192-column sparse tiles (config 5's shape) may run in cooperative record groups of
+// 1 << SPG_SP_RGS tiles (k_tile_sp<.., RG>; A/B builds).  Measured on config 5 (round 5): RG 4
+// cut the numeric kernel's fabric reads from 511 to 361 GB per launch but took 103 ms against
+// 97 ms for RG 1 (RG 2: 100 ms, RG 8: 103 ms) -- the block's waves wait for its slowest item --
+// so the shipped build keeps RG = 1 (plain tile-major records)
 #ifndef SPG_SP_RGS
-#define SPG_SP_RGS 2
+#define SPG_SP_RGS 0
 #endif
 // (SPG_SP_RECORD_GROUP=1, read per plan: a schedule-only switch to the one-wave kernel over
 // plain tile-major records, for A/B timing and for the tests; results are identical)
@@ -955,15 +972,8 @@ spg_status_t tile_sym_chunk(spg_handle_t h, spg_plan_s& p, int64_t c) {
                          dim3(SEG_WPB * WAVE), r0, n, p.tws, p.G, p.twss, (const IP*)p.A.indptr,
                          (const int32_t*)p.A.indices, (const IP*)p.B.indptr, (const uint16_t*)p.bj16,
                          (const uint32_t*)p.sidx, tile_dense(p) ? (uint32_t*)nullptr : p.bitmap, items);
-        else if (SPG_SYM8 && SPG_SYM_CO > 1 && sym_tiles(p) >= SPG_SYM_CO && !sym_co_off())
-            // cooperative blocks: SPG_SYM_CO symbolic tiles of one row per block
-            timed_launch(h, SPG_PHASE_SYMBOLIC, k_tile_sym8<IP, SPG_SYM_CO>,
-                         dim3(coop_grid(n * ((sym_tiles(p) + SPG_SYM_CO - 1) / SPG_SYM_CO), SPG_SYM_CO)), dim3(SPG_SYM_CO * WAVE),
-                         r0, n, p.tws, p.G, p.twss, (const IP*)p.A.indptr, (const int32_t*)p.A.indices,
-                         (const IP*)p.B.indptr, (const uint16_t*)p.bj16, (const uint32_t*)p.sidx,
-                         tile_dense(p) ? (uint32_t*)nullptr : p.bitmap, items);
         else if (SPG_SYM8)
-            timed_launch(h, SPG_PHASE_SYMBOLIC, k_tile_sym8<IP, 1>, dim3(tile_grid(n * sym_tiles(p))), dim3(TILE_WPB * WAVE),
+            timed_launch(h, SPG_PHASE_SYMBOLIC, k_tile_sym8<IP>, dim3(tile_grid(n * sym_tiles(p))), dim3(TILE_WPB * WAVE),
                          r0, n, p.tws, p.G, p.twss, (const IP*)p.A.indptr, (const int32_t*)p.A.indices,
                          (const IP*)p.B.indptr, (const uint16_t*)p.bj16, (const uint32_t*)p.sidx,
                          tile_dense(p) ? (uint32_t*)nullptr : p.bitmap, items);
@@ -1080,6 +1090,17 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
                                   dense ? (const uint32_t*)nullptr : (const uint32_t*)p.bitmap,
                                   (const int64_t*)tile_chunk_items(p, c), cj, cx, alpha, it_lo, it_hi, p.rgs);
         };
+        if constexpr (std::is_same<T, float>::value) {
+            if (dense && p.lean && fp32_runs(p)) {   // fp32 dense tiles of long B segments: entry runs
+                hipExtLaunchKernelGGL((k_tile_dn<T, IP, 1024>), dim3(tile_grid(nit, DN_WPB)), dim3(DN_WPB * WAVE),
+                                      0, h->stream, kt.a, kt.b, 0, r0, n, p.tws, p.G, Ap, Aj, Ax, p.B.rows,
+                                      (const uint32_t*)p.brec, (const int32_t*)p.tptr,
+                                      (const int64_t*)tile_chunk_items(p, c), cj, cx, alpha,
+                                      sent(sentinel_region(1024)), it_lo, it_hi, p.rgs);
+                SPG_LAUNCHED(h);
+                continue;
+            }
+        }
         if constexpr (OrderedLdsAdd<T>::value) {
             if (!dense && p.lean && SPG_SP_LEAN) {   // sparse tiles, ordered LDS adds
                 auto sp = [&](auto cfg, auto rgc) {
@@ -1099,10 +1120,17 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
                 };
                 using One = std::integral_constant<int, 1>;
                 if constexpr (std::is_same<T, double>::value) {
-                    if (p.tws > 12 && p.rgs == SPG_SP_RGS && SPG_SP_RGS > 0)
-                        sp(SpCfgRG{}, std::integral_constant<int, (1 << SPG_SP_RGS)>{});
-                    else if (p.tws > 12) sp(SpCfg2048{}, One{});
-                    else sp(SpCfg1024{}, One{});
+                    bool done = false;
+                    if constexpr (SPG_SP_RGS > 0) {
+                        if (p.tws > 12 && p.rgs == SPG_SP_RGS) {
+                            sp(SpCfgRG{}, std::integral_constant<int, (1 << SPG_SP_RGS)>{});
+                            done = true;
+                        }
+                    }
+                    if (!done) {
+                        if (p.tws > 12) sp(SpCfg2048{}, One{});
+                        else sp(SpCfg1024{}, One{});
+                    }
                 } else {
                     sp(SpCfg1024{}, One{});
                 }

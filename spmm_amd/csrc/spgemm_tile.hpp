@@ -497,19 +497,13 @@ struct Sym8Lds {
 #ifndef SPG_SYM8_WPE
 #define SPG_SYM8_WPE 1   // (A/B: a waves-per-SIMD floor for k_tile_sym8's register budget)
 #endif
-// CO = 1: two-wave blocks, one task (row, symbolic tile) per wave.  CO > 1 (round 5): blocks
-// of CO waves take CO consecutive symbolic tiles of ONE row (wave w: symbolic tile q*CO + w),
-// with a barrier per row: a B row's segments of adjacent symbolic tiles are adjacent in Bj16,
-// so the block's waves read one contiguous run per A entry (config 5: four 131-byte segments,
-// ~2 lines each alone, ~5 lines together) and the lines they share are fetched once.
-template <typename IP, int CO>
-__global__ __launch_bounds__((CO > 1 ? CO : TILE_WPB) * WAVE) __attribute__((amdgpu_waves_per_eu(SPG_SYM8_WPE))) void k_tile_sym8(
+template <typename IP>
+__global__ __launch_bounds__(TILE_WPB * WAVE) __attribute__((amdgpu_waves_per_eu(SPG_SYM8_WPE))) void k_tile_sym8(
     int64_t row0, int64_t nrows, int tws, int G, int twss, const IP* __restrict__ Ap,
     const int32_t* __restrict__ Aj, const IP* __restrict__ Bp, const uint16_t* __restrict__ Bj16,
     const uint32_t* __restrict__ sidx, uint32_t* __restrict__ bitmap, int64_t* __restrict__ item_cnt) {
     constexpr int U = 8;   // chunks of 64 words in flight
-    constexpr int WPB = CO > 1 ? CO : TILE_WPB;
-    __shared__ __attribute__((aligned(16))) Sym8Lds lds[WPB];
+    __shared__ __attribute__((aligned(16))) Sym8Lds lds[TILE_WPB];
     const int l = lane_id();
     const int wv = uniform((int)(threadIdx.x >> 6));
     Sym8Lds& S = lds[wv];
@@ -517,15 +511,11 @@ __global__ __launch_bounds__((CO > 1 ? CO : TILE_WPB) * WAVE) __attribute__((amd
     const int nw = (1 << tws) >> 5;           // bitmap words of a numeric tile
     const int R = 1 << (twss - tws);          // numeric tiles per symbolic tile
     const int Gs = (G + R - 1) / R;           // symbolic tiles per row
-    const int Gc = CO > 1 ? (Gs + CO - 1) / CO : Gs;   // tasks per row (CO > 1: groups of CO tiles)
-    const uint32_t tasks = (uint32_t)(nrows * Gc);
-    const uint32_t stride = CO > 1 ? gridDim.x : gridDim.x * TILE_WPB;
-    for (uint32_t task = (CO > 1 ? xcd_block(gridDim.x) : xcd_block(gridDim.x) * TILE_WPB + wv); task < tasks;
-         task += stride) {
-        if constexpr (CO > 1) __syncthreads();   // the block's waves start every row together
-        const int64_t row = row0 + (int64_t)(task / (uint32_t)Gc);
-        const int gs = CO > 1 ? (int)(task % (uint32_t)Gc) * CO + wv : (int)(task % (uint32_t)Gc);
-        if (CO > 1 && gs >= Gs) continue;        // (past the row's last symbolic tile)
+    const uint32_t tasks = (uint32_t)(nrows * Gs);
+    const uint32_t stride = gridDim.x * TILE_WPB;
+    for (uint32_t task = xcd_block(gridDim.x) * TILE_WPB + wv; task < tasks; task += stride) {
+        const int64_t row = row0 + (int64_t)(task / (uint32_t)Gs);
+        const int gs = (int)(task % (uint32_t)Gs);
         const int t0 = gs * R, t1 = min(G, t0 + R);
         const int lo16 = (t0 << tws) & 0xffff;
         const int nws = (t1 - t0) * nw;

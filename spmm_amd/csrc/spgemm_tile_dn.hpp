@@ -41,18 +41,19 @@ template <typename R> __device__ __forceinline__ void lds_add(cplx<R>* p, cplx<R
 }
 
 // Run-time check of the two properties above (spg_create, lds_order_check in spgemm.hip):
-// LDSCHK_TRIALS trials; in each, two ds_add_f64 instructions from all 64 lanes into 4 slots
-// (v and slot indexed [trial][instruction][lane]); the slots' sums go to out[trial][4].
+// LDSCHK_TRIALS trials; in each, two ds_add_f64 (ds_add_f32) instructions from all 64 lanes into 4
+// slots (v and slot indexed [trial][instruction][lane]); the slots' sums go to out[trial][4].
 constexpr int LDSCHK_TRIALS = 64;
-__global__ __launch_bounds__(WAVE) void k_lds_order_check(const double* __restrict__ v, const int* __restrict__ slot,
-                                                          double* __restrict__ out) {
-    __shared__ double acc[4];
+template <typename T>
+__global__ __launch_bounds__(WAVE) void k_lds_order_check(const T* __restrict__ v, const int* __restrict__ slot,
+                                                          T* __restrict__ out) {
+    __shared__ T acc[4];
     const int l = lane_id();
     for (int t = 0; t < LDSCHK_TRIALS; ++t) {
-        if (l < 4) acc[l] = 0.0;
+        if (l < 4) acc[l] = (T)0;
         wsync();
         const int i0 = t * 2 * WAVE + l, i1 = i0 + WAVE;
-        const double v0 = v[i0], v1 = v[i1];
+        const T v0 = v[i0], v1 = v[i1];
         const int s0 = slot[i0], s1 = slot[i1];
         lds_add(&acc[s0], v0);
         lds_add(&acc[s1], v1);
@@ -104,6 +105,7 @@ template <typename T> struct __attribute__((aligned(16))) DnEnt {
     T a;
 };
 
+
 // fp64 items take their structure from the accumulator itself (SPG_DN_SENT): every slot
 // starts at -0.0 instead of +0.0.  -0.0 + p == +0.0 + p for every p except p == -0.0, so a
 // column's sum equals scipy's (which starts at +0.0) except while every product it has seen
@@ -148,6 +150,7 @@ template <typename T, int TWD> struct DnLds<T, TWD, false> {
     uint8_t pad[SPG_LDS_PAD];   // (A/B builds: occupancy sensitivity)
 #endif
 };
+
 
 // Markers of one group of 8 chunks (transposed as num_group_markers): entry l's first product
 // gets l + 1, and product Pb (the batch's end, if inside the group) the pseudo entry's WAVE + 1.
@@ -279,8 +282,34 @@ __device__ __forceinline__ void dn_walk(L* lp, T* acc, int l, const int32_t* __r
                             acc[c] = mul_rn(qa[u], qv[u]);
                         } else if constexpr ((SPG_TILE_DIAG & 32) != 0) {   // timing only: conflict-free adds
                             lds_add(&acc[l + (c & 1)], mul_rn(qa[u], qv[u]));
-                        } else if constexpr ((SPG_TILE_DIAG & 1) == 0) {   // (diag 1, timing only: no accumulation)
+                        } else if constexpr ((SPG_TILE_DIAG & 1) == 0 && OrderedLdsAdd<T>::value) {   // (diag 1: none)
                             lds_add(&acc[c], mul_rn(qa[u], qv[u]));   // chunk order = issue order
+                            hit(c);
+                        } else if constexpr ((SPG_TILE_DIAG & 1) == 0) {
+                            // fp32 (round 5): ds_add_f32 costs 193 CU-cycles per wave instruction on
+                            // MI355X, a plain read-add-write 17.  The products of ONE A entry in a
+                            // chunk hit distinct columns (a B row's columns are distinct), so the
+                            // chunk's run of each entry (sp[u], non-decreasing over the lanes) adds
+                            // with a plain read-add-write, runs in entry order; a chunk holding more
+                            // than two entries adds its third and later runs with one ordered
+                            // ds_add_f32 (ascending lanes = entry order).  Lanes past the batch
+                            // (pseudo entry) add nothing.
+                            const T pv = mul_rn(qa[u], qv[u]);
+                            bool live = sp[u] <= (unsigned)WAVE;
+                            for (int run = 0;; ++run) {
+                                const unsigned long long m = __ballot(live);
+                                if (m == 0ull) break;
+                                if (run == 2) {
+                                    if (live) lds_add(&acc[c], pv);
+                                    break;
+                                }
+                                const unsigned e0 = (unsigned)readlane_i((int)sp[u], (int)__builtin_ctzll(m));
+                                if (live && sp[u] == e0) {
+                                    acc[c] = add_rn(acc[c], pv);
+                                    live = false;
+                                }
+                                __builtin_amdgcn_wave_barrier();
+                            }
                             hit(c);
                         }
                     }
@@ -398,7 +427,7 @@ __global__ __launch_bounds__(DN_WPB * WAVE) void k_tile_dn(
     const uint32_t* __restrict__ brec, const int32_t* __restrict__ tptr,
     const int64_t* __restrict__ item_off, int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha, uint32_t sent,
     uint32_t it_lo, uint32_t it_hi, int rgs) {
-    static_assert(OrderedLdsAdd<T>::value, "ordered LDS add needed");
+    static_assert(OrderedLdsAdd<T>::value || std::is_same<T, float>::value, "ordered LDS add or fp32 runs");
     constexpr int NB = sizeof(T) > 8 ? 4 : 8;    // A batches preloaded per item
     __shared__ __attribute__((aligned(16))) DnLds<T, TWD> lds[DN_WPB];
     const int l = lane_id();
@@ -458,9 +487,10 @@ template <int CAP_, int NW_, int DUMMY_, int MKB_> struct SpCfg {
 };
 using SpCfg1024 = SpCfg<1024, 128, WAVE, 8>;    // tiles of <= 4096 columns (11.3 KB per wave)
 using SpCfg2048 = SpCfg<2048, 256, WAVE, 16>;   // fp64 8192-column tiles (21.0 KB)
-// fp64 8192-column tiles in cooperative blocks of 4 waves (k_tile_sp<.., RG = 4>): 20,432 bytes per
-// wave, so two 4-wave blocks (8 waves) fit a CU's 160 KB; 2032 slots per window (config 5's
-// items hold 1887 +- 40 entries) and 8 lane slots (an out-of-window add conflicts at most 8 ways)
+// fp64 8192-column tiles in cooperative blocks of RG waves (k_tile_sp<.., RG>, A/B builds with
+// SPG_SP_RGS > 0): 20,432 bytes per wave, so two 4-wave blocks (8 waves) fit a CU's 160 KB;
+// 2032 slots per window (config 5's items hold 1887 +- 40 entries) and 8 lane slots (an
+// out-of-window add conflicts at most 8 ways)
 using SpCfgRG = SpCfg<2032, 256, 8, 16>;
 template <typename T, typename CF> struct SpLds {
     T acc[CF::CAP + CF::DUMMY];         // compact accumulator of one window; + lane slots

@@ -359,11 +359,10 @@ def _random_rows(rng, rows, cols, per_row):
 
 
 def test_tile_path_cooperative_groups_with_padding():
-    """Config 5's cooperative kernels on a shape whose group counts do not divide: 300000
-    columns -> 37 numeric tiles of 8192 (record groups of 4: the last holds 1 real tile and 3
-    padding tiles) and 5 symbolic tiles of 65536 (k_tile_sym8 blocks of 4: the second block
-    has 1 real symbolic tile).  Bit-exact for ALG2 and chunked ALG3, and the same with both
-    cooperative schedules switched off (SPG_SP_RECORD_GROUP=1, SPG_SYM_COOP=0)."""
+    """Config 5's 8192-column sparse tiles on a shape whose tile count does not divide by 4:
+    300000 columns -> 37 numeric tiles (A/B builds with cooperative record groups of 4: the last
+    group holds 1 real tile and 3 padding tiles), 5 symbolic tiles of 65536.  Bit-exact for ALG2
+    and chunked ALG3, and the same with the one-wave kernel (SPG_SP_RECORD_GROUP=1)."""
     from spmm_amd import cusparse
     from spmm_amd.sparse import csr_matrix
     rng = np.random.default_rng(39)
@@ -372,16 +371,15 @@ def test_tile_path_cooperative_groups_with_padding():
     B = _random_rows(rng, n, n, 60)
     dA, dB = csr_matrix(A, device=_dev()), csr_matrix(B, device=_dev())
     info = cusparse.plan_info(dA, dB, alg=2)
-    assert info["tile_width"] == 8192 and info["tiles_per_row"] == 37 and info["record_group"] == 4, info
+    assert info["tile_width"] == 8192 and info["tiles_per_row"] == 37 and info["record_group"] in (1, 4), info
     ref = oracle.spgemm(A, B, alpha=1.5, keep_zeros=True, sort=True, threads=16)
     for alg, cf in [(2, 0.2), ("3c", 0.1)]:
         _assert_same(_gpu(A, B, alg=alg, alpha=1.5, cf=cf), ref)
     os.environ["SPG_SP_RECORD_GROUP"] = "1"
-    os.environ["SPG_SYM_COOP"] = "0"
     try:
         _assert_same(_gpu(A, B, alg=2, alpha=1.5), ref)
     finally:
-        del os.environ["SPG_SP_RECORD_GROUP"], os.environ["SPG_SYM_COOP"]
+        del os.environ["SPG_SP_RECORD_GROUP"]
 
 
 def test_tile_path_sparse_8192():
@@ -405,9 +403,9 @@ def test_tile_path_sparse_8192():
     dA, dB = csr_matrix(A, device=_dev()), csr_matrix(B, device=_dev())
     info = cusparse.plan_info(dA, dB, alg=2)
     assert info["tile_width"] == 8192 and not info["dense_tiles"], info
-    # cooperative record groups of 4 tiles (k_tile_sp<.., SpCfgRG, 4>): G = 5 tiles, so the
-    # second group holds one real tile and three padding tiles
-    assert info["record_group"] == 4 and info["tiles_per_row"] == 5, info
+    # (A/B builds with cooperative record groups of 4 tiles: G = 5 tiles, so the second group
+    # holds one real tile and three padding tiles)
+    assert info["record_group"] in (1, 4) and info["tiles_per_row"] == 5, info
     ref = oracle.spgemm(A, B, alpha=0.5, keep_zeros=True, sort=True)
     assert np.diff(ref[0]).max() > 2 * 2048 * 4   # dense rows: several windows per item
     for alg, cf in [(1, 0.2), (2, 0.2), (3, 0.2), ("3c", 0.02)]:
@@ -784,3 +782,28 @@ def test_tile_dense_negative_zero_products(frac, dtype):
     B.data = np.where(rng.random(B.nnz) < frac, dtype(-0.0), B.data).astype(dtype)
     for alg in (1, 2):
         _assert_same(_gpu(A, B, alg=alg), oracle.spgemm(A, B, keep_zeros=True, sort=True))
+
+
+@pytest.mark.parametrize("n,density,neg", [(4096, 0.1, 0.0), (2048, 0.2, 0.3), (4096, 0.05, 0.0)])
+def test_tile_fp32_entry_runs(n, density, neg):
+    """fp32 dense tiles whose B segments hold >= 48 entries per 1024-column tile run
+    k_tile_dn<float, .., 1024>: each A entry's run of a 64-product chunk adds with a plain LDS
+    read-add-write (its columns are distinct), runs in entry order, the third and later runs of a
+    chunk with one ordered ds_add_f32 (config 3 at density 0.1: 102-entry segments; 0.05: 51).
+    Bit-exact against the oracle for ALG1 / ALG2 / chunked ALG3 and alpha != 1, with `neg` of
+    B's values set to -0.0 (the -0.0 accumulator start and its re-walk), and equal to k_tile's
+    owner rounds (SPG_F32_RUNS=0)."""
+    from spmm_amd import gen
+    A, B = gen.scipy_pair(n, density, seed=7, dtype=np.float32)
+    if neg:
+        A.data = np.abs(A.data) + np.float32(0.5)
+        rng = np.random.default_rng(2)
+        B.data = np.where(rng.random(B.nnz) < neg, np.float32(-0.0), B.data).astype(np.float32)
+    ref = oracle.spgemm(A, B, alpha=1.5, keep_zeros=True, sort=True, threads=16)
+    for alg, cf in [(1, 0.2), (2, 0.2), ("3c", 0.1)]:
+        _assert_same(_gpu(A, B, alg=alg, alpha=1.5, cf=cf), ref)
+    os.environ["SPG_F32_RUNS"] = "0"
+    try:
+        _assert_same(_gpu(A, B, alg=2, alpha=1.5), ref)
+    finally:
+        del os.environ["SPG_F32_RUNS"]

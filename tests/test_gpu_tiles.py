@@ -174,10 +174,13 @@ for name, alg in runs:
     (r0, r1), A_blk, _ = distributed.rowblock_setup(dA, dA.indptr.new_tensor(B.indptr), world, rank)
     C, _ = distributed.rowblock_step(A_blk, B_src, 0, dev, alg=alg, pipeline=True, n_groups=3)
     torch.cuda.synchronize()
+    from spmm_amd import cusparse
+    info = cusparse.plan_info(A_blk, csr_matrix(B, device=dev), alg=2)
     tv = distributed.rowblock_step.last
     np.savez(os.path.join(OUT, f"{name}_alg{alg}_{rank}.npz"), p=C.indptr.cpu().numpy().astype(np.int64),
              j=C.indices.cpu().numpy(), x=C.data.cpu().numpy(), rows=np.array([r0, r1]),
-             pipelined=np.array([tv.pipelined]), groups=np.array(tv.groups).reshape(-1, 2))
+             pipelined=np.array([tv.pipelined]), groups=np.array(tv.groups).reshape(-1, 2),
+             value_tiles=np.array([-(-info["tiles_per_row"] // max(1, info["record_group"]))]))
 dist.destroy_process_group()
 """
 
@@ -208,8 +211,9 @@ def test_pipelined_rowblock_two_ranks_one_gpu(tmp_path):
                       ("sparse8192_f64", 3)]:
         _, A, B, alpha = cases[name]
         parts = [np.load(tmp_path / f"{name}_alg{alg}_{r}.npz") for r in range(2)]
-        if alg == 2:   # pipelined: 3 tile groups on both ranks
-            assert all(bool(q["pipelined"][0]) and len(q["groups"]) == 3 for q in parts), (name, alg)
+        if alg == 2:   # pipelined: 3 value-tile groups on both ranks (fewer value tiles: one each)
+            assert all(bool(q["pipelined"][0]) and len(q["groups"]) == min(3, int(q["value_tiles"][0]))
+                       for q in parts), (name, alg)
         else:          # the fallback: one row-major values broadcast, spg_numeric
             assert not any(bool(q["pipelined"][0]) for q in parts), (name, alg)
         p = distributed.stitch_indptr([q["p"] for q in parts], [len(q["j"]) for q in parts])
