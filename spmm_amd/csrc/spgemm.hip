@@ -293,6 +293,15 @@ inline int sym_tile_log2(const spg_csr_t& B, int tws, bool* seg = nullptr) {
 }
 
 
+// C rows expected full (1 - exp(-avgA * avgB / N) >= 0.999, e.g. config 3 at density 0.1): the
+// segment-walking symbolic kernel stops a task once its bitmap is full (a pure shortcut: the
+// structure it writes is the same)
+inline bool sym_full(const spg_plan_s& p) {
+    if (p.A.rows <= 0 || p.B.rows <= 0 || p.B.cols <= 0) return false;
+    const double avgA = (double)p.A.nnz / (double)p.A.rows, avgB = (double)p.B.nnz / (double)p.B.rows;
+    return avgA * avgB / (double)p.B.cols >= 6.9;
+}
+
 // Makes the handle's device current for one entry point and restores the caller's device
 // on exit (cuSPARSE leaves the current device alone; so does this library).
 struct DeviceGuard {
@@ -971,7 +980,8 @@ spg_status_t tile_sym_chunk(spg_handle_t h, spg_plan_s& p, int64_t c) {
             timed_launch(h, SPG_PHASE_SYMBOLIC, k_tile_sym_seg<IP>, dim3(tile_grid(n * sym_tiles(p), SEG_WPB)),
                          dim3(SEG_WPB * WAVE), r0, n, p.tws, p.G, p.twss, (const IP*)p.A.indptr,
                          (const int32_t*)p.A.indices, (const IP*)p.B.indptr, (const uint16_t*)p.bj16,
-                         (const uint32_t*)p.sidx, tile_dense(p) ? (uint32_t*)nullptr : p.bitmap, items);
+                         (const uint32_t*)p.sidx, tile_dense(p) ? (uint32_t*)nullptr : p.bitmap, items,
+                         sym_full(p) ? p.B.cols : (int64_t)0);
         else if (SPG_SYM8)
             timed_launch(h, SPG_PHASE_SYMBOLIC, k_tile_sym8<IP>, dim3(tile_grid(n * sym_tiles(p))), dim3(TILE_WPB * WAVE),
                          r0, n, p.tws, p.G, p.twss, (const IP*)p.A.indptr, (const int32_t*)p.A.indices,

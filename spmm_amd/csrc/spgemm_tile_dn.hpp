@@ -296,6 +296,28 @@ __device__ __forceinline__ void dn_walk(L* lp, T* acc, int l, const int32_t* __r
                             // (pseudo entry) add nothing.
                             const T pv = mul_rn(qa[u], qv[u]);
                             bool live = sp[u] <= (unsigned)WAVE;
+                            // two runs whose column ranges do not overlap (a segment's tail in
+                            // high columns, the next segment's head in low ones -- most chunks
+                            // that hold a segment boundary) are distinct too: one read-add-write
+                            const unsigned long long lm = __ballot(live);   // live lanes: a prefix
+                            if (lm != 0ull) {
+                                const unsigned e0 = (unsigned)readlane_i((int)sp[u], 0);
+                                const unsigned long long m2 = __ballot(live && sp[u] != e0);
+                                bool one = m2 == 0ull;
+                                if (!one) {
+                                    const int l2 = (int)__builtin_ctzll(m2), last = 63 - (int)__builtin_clzll(lm);
+                                    const unsigned e1 = (unsigned)readlane_i((int)sp[u], l2);
+                                    if (__ballot(live && sp[u] != e0 && sp[u] != e1) == 0ull) {
+                                        const int c1 = readlane_i(c, 0), ck = readlane_i(c, l2 - 1);
+                                        const int d1 = readlane_i(c, l2), dm = readlane_i(c, last);
+                                        one = dm < c1 || d1 > ck;
+                                    }
+                                }
+                                if (one) {
+                                    if (live) acc[c] = add_rn(acc[c], pv);
+                                    live = false;
+                                }
+                            }
                             for (int run = 0;; ++run) {
                                 const unsigned long long m = __ballot(live);
                                 if (m == 0ull) break;
@@ -687,11 +709,16 @@ void k_tile_sp(
 // k_tile_sym.  (Measured on config 4: 4.05 ms against 7.05 ms for k_tile_sym's flattened
 // walk over 16384-column tiles and 7.0 ms for a one-entry-per-instruction cursor walk.)
 constexpr int SEG_WPB = 2;
+// `ncols` > 0 (plans whose C rows are expected to be full, SPG_SYM_FULL in spgemm.hip): every 64
+// A entries the wave counts its bitmap, and a task whose columns [lo, min(lo + width, ncols))
+// are all set stops walking -- later products cannot add a column (config 3 at density 0.1:
+// C rows 100 % dense, ~90 of 819 A entries fill a row).
 template <typename IP>
 __global__ __launch_bounds__(SEG_WPB * WAVE) void k_tile_sym_seg(
     int64_t row0, int64_t nrows, int tws, int G, int twss, const IP* __restrict__ Ap,
     const int32_t* __restrict__ Aj, const IP* __restrict__ Bp, const uint16_t* __restrict__ Bj16,
-    const uint32_t* __restrict__ sidx, uint32_t* __restrict__ bitmap, int64_t* __restrict__ item_cnt) {
+    const uint32_t* __restrict__ sidx, uint32_t* __restrict__ bitmap, int64_t* __restrict__ item_cnt,
+    int64_t ncols) {
     constexpr int NQ = 4;   // quads of A entries per round: 16 entries, 4 loads in flight per lane
     __shared__ __attribute__((aligned(16))) uint32_t bits_all[SEG_WPB][SYM_NWMAX];
     const int l = lane_id();
@@ -745,7 +772,16 @@ __global__ __launch_bounds__(SEG_WPB * WAVE) void k_tile_sym_seg(
         int cnt[NQ];
         int64_t beg[NQ];
         extents(0, cnt, beg);
+        // the task's valid columns (the last tile of a row may pass the matrix's last column)
+        const int full = ncols > 0 ? (int)min((int64_t)nws * 32, ncols - ((int64_t)t0 << tws)) : 0;
         for (int b = 0; b < nA; b += 4 * NQ) {
+            if (full > 0 && b > 0 && (b & (WAVE - 1)) == 0) {   // every 64 entries: full yet?
+                wsync();
+                int c = 0;
+                for (int w = l; w < nws; w += WAVE) c += __popc(bits[w]);
+                c = wave_incl_sum_dpp(c);
+                if (readlane_i(c, WAVE - 1) >= full) break;
+            }
             // eight 16-bit columns per lane per 16-byte load: each segment from its 8-aligned
             // start (span = cnt + (beg & 7) elements; an element before beg or past the segment
             // is skipped; the region is padded, so the last load stays inside it).  A 16-lane
