@@ -636,6 +636,30 @@ def run_alg3_chunked(ctx, args, tdt, n=262144, dens=1e-3, cf=0.02, steps=2, warm
     return out
 
 
+def run_config3_fp32(ctx, args, n=8192, dens=0.1, steps=10, warmup=2):
+    """BASELINE config 3's densest point in fp32, the dtype of every published reference figure
+    (SpGEMM_alg_comparison/profiler.py:215-222, dense_vs_sparseGEMM/utils.py:278-289): one
+    C = A.B at N=8192, density 0.1 (ALG2), with its phases.  rocBLAS sgemm on the same N takes
+    7.2 ms (profiles/r03_dense_vs_sparse_fp32.txt) -- the break-even the reference's
+    dense_vs_sparseGEMM sweep looks for."""
+    from spmm_amd import cusparse
+    torch = ctx.torch
+    A = gen_device(ctx, n, dens, args.seed, torch.float32)
+    B = gen_device(ctx, n, dens, args.seed + 1, torch.float32)
+    P = cusparse.num_products(A, B)
+    elapsed, C = timed(ctx, lambda: cusparse.spgemm(A, B, alg=2), steps, warmup)
+    del C
+    ph = phase_times(ctx, lambda: cusparse.spgemm(A, B, alg=2), 2)
+    kname, _ = tile_kernel(ctx, A, B, 2, 0.2)
+    out = {"N": n, "density": dens, "dtype": "f32", "alg": 2, "num_products": int(P),
+           "ms_per_step": round(elapsed / steps * 1e3, 4), "gflops": round(2.0 * P * steps / elapsed / 1e9, 3),
+           "kernel": kname, "phases_ms_per_step": {k: round(v[0] / 2, 5) for k, v in ph.items() if v[1]},
+           "sgemm_ms_same_n": 7.2}
+    del A, B
+    torch.cuda.empty_cache()
+    return out
+
+
 def run_config2(ctx, args, cfg, npdt, vb, with_cpu):
     """Config 2 (ALG1, N=16384) on one GPU: GFLOPS, its k_row roofline and the other ALGs."""
     from spmm_amd import _lib, cusparse, gen
@@ -702,6 +726,8 @@ def main(argv=None):
             line["config2"] = run_config2(ctx, args, CONFIGS["2"], npdt, vb, with_cpu=False)
         if ctx.world == 1 and ctx.gpu and not args.no_alg3_chunked:
             line["alg3_chunked"] = run_alg3_chunked(ctx, args, tdt)
+        if ctx.world == 1 and ctx.gpu and not args.no_config2:
+            line["config3_fp32"] = run_config3_fp32(ctx, args)
         if ctx.world > 1 and args.config5_n > 0:
             line["config5"] = run_config5(ctx, args, CONFIGS["5"], args.config5_n, tdt, vb, hook,
                                           steps=3, warmup=1)

@@ -187,6 +187,10 @@ inline bool row_kernel_enabled() {
 #ifndef SPG_SYM8
 #define SPG_SYM8 1
 #endif
+//   SPG_SYM8_CW     waves per k_tile_sym8 task sharing one bitmap (1: k_tile_sym8, one wave per task)
+#ifndef SPG_SYM8_CW
+#define SPG_SYM8_CW 2
+#endif
 #ifndef SPG_TILE_LEAN
 #define SPG_TILE_LEAN 1
 #endif
@@ -632,17 +636,27 @@ inline bool fp32_runs(const spg_plan_s& p) {
     const double seg = (double)p.B.nnz / (double)p.B.rows * (double)(1 << p.tws) / (double)p.B.cols;
     return seg >= SPG_F32_RUN_MIN;
 }
-// fp64 8192-column sparse tiles (config 5's shape) may run in cooperative record groups of
-// 1 << SPG_SP_RGS tiles (k_tile_sp<.., RG>; A/B builds).  Measured on config 5 (round 5): RG 4
-// cut the numeric kernel's fabric reads from 511 to 361 GB per launch but took 103 ms against
-// 97 ms for RG 1 (RG 2: 100 ms, RG 8: 103 ms) -- the block's waves wait for its slowest item --
-// so the shipped build keeps RG = 1 (plain tile-major records)
+// fp64 8192-column sparse tiles (config 5's shape) run in cooperative record groups of
+// 1 << SPG_SP_RGS tiles (k_tile_sp<.., RG>), on a persistent grid of 8 / RG blocks per CU.
+// Measured on config 5 (round 5, numeric ms per product): RG 1 97.6 (511 GB of fabric reads per
+// launch); RG 4 with one block per item 103 (361 GB: the block's waves idle until its slowest
+// item ends, and a new block needs a whole block's LDS); RG 4 persistent 92.7 (367 GB), RG 8
+// persistent 91.8, RG 2 persistent 101.3; RG 1 persistent 118.5 (one-wave blocks balance best
+// dispatched one item each).  SPG_SP_RGS=0 builds keep RG = 1.
 #ifndef SPG_SP_RGS
-#define SPG_SP_RGS 0
+#define SPG_SP_RGS 2
 #endif
 // (SPG_SP_RECORD_GROUP=1, read per plan: a schedule-only switch to the one-wave kernel over
 // plain tile-major records, for A/B timing and for the tests; results are identical)
+// (SPG_DN_RGS = 1, A/B builds: fp64 2048-column dense tiles in record groups of 2, one per
+// 2-wave block of k_tile_dn<.., RG = 2> on a persistent grid; config 4 numeric 22.4 ms against
+// 19.1 ms for independent items, round 5)
+#ifndef SPG_DN_RGS
+#define SPG_DN_RGS 0
+#endif
 inline int record_group_log2(const spg_plan_s& p) {
+    if (SPG_DN_RGS > 0 && p.use_tile && tile_dense(p) && p.lean && p.A.value_type == SPG_R_64F && p.tws == 11)
+        return SPG_DN_RGS;
     if (!p.use_tile || tile_dense(p) || !p.lean || !SPG_SP_LEAN) return 0;
     if (p.A.value_type != SPG_R_64F || p.tws != 13) return 0;
     const char* e = std::getenv("SPG_SP_RECORD_GROUP");
@@ -982,6 +996,12 @@ spg_status_t tile_sym_chunk(spg_handle_t h, spg_plan_s& p, int64_t c) {
                          (const int32_t*)p.A.indices, (const IP*)p.B.indptr, (const uint16_t*)p.bj16,
                          (const uint32_t*)p.sidx, tile_dense(p) ? (uint32_t*)nullptr : p.bitmap, items,
                          sym_full(p) ? p.B.cols : (int64_t)0);
+        else if (SPG_SYM8 && SPG_SYM8_CW > 1)   // shared bitmap, SPG_SYM8_CW waves per task
+            timed_launch(h, SPG_PHASE_SYMBOLIC, k_tile_sym8c<IP, SPG_SYM8_CW>,
+                         dim3(coop_grid(n * sym_tiles(p), SPG_SYM8_CW)), dim3(SPG_SYM8_CW * WAVE),
+                         r0, n, p.tws, p.G, p.twss, (const IP*)p.A.indptr, (const int32_t*)p.A.indices,
+                         (const IP*)p.B.indptr, (const uint16_t*)p.bj16, (const uint32_t*)p.sidx,
+                         tile_dense(p) ? (uint32_t*)nullptr : p.bitmap, items);
         else if (SPG_SYM8)
             timed_launch(h, SPG_PHASE_SYMBOLIC, k_tile_sym8<IP>, dim3(tile_grid(n * sym_tiles(p))), dim3(TILE_WPB * WAVE),
                          r0, n, p.tws, p.G, p.twss, (const IP*)p.A.indptr, (const int32_t*)p.A.indices,
@@ -1122,7 +1142,10 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
                         it_hi = (uint32_t)(q1 * n);
                         nit = (q1 - q0) * n;
                     }
-                    hipExtLaunchKernelGGL((k_tile_sp<T, IP, CF, RG>), dim3(coop_grid(nit, RG)), dim3(RG * WAVE),
+                    // RG > 1: a persistent grid, 8 / RG blocks per CU (the LDS holds 8 such waves)
+                    const unsigned spg_grid = RG > 1 ? (unsigned)std::min<int64_t>(coop_grid(nit, RG), (int64_t)h->cus * 8 / RG)
+                                                     : coop_grid(nit, RG);
+                    hipExtLaunchKernelGGL((k_tile_sp<T, IP, CF, RG>), dim3(spg_grid), dim3(RG * WAVE),
                                           0, h->stream, kt.a, kt.b, 0, r0, n, p.tws, p.G, Ap, Aj, Ax, p.B.rows,
                                           (const uint32_t*)p.brec, (const int32_t*)p.tptr, (const uint32_t*)p.bitmap,
                                           (const int64_t*)tile_chunk_items(p, c), cj, cx, alpha,
@@ -1150,6 +1173,18 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
             if (dense && p.lean) {   // ordered LDS adds (spgemm_tile_dn.hpp)
                 auto dn = [&](auto twd) {
                     constexpr int TWD = decltype(twd)::value;
+                    if constexpr (SPG_DN_RGS > 0 && TWD == 2048) {
+                        if (p.rgs == SPG_DN_RGS) {   // record groups of DN_WPB tiles, one per block
+                            const int64_t q0 = g0 >> p.rgs, q1 = (g1 + DN_WPB - 1) >> p.rgs;
+                            const unsigned gd = (unsigned)std::min<int64_t>(coop_grid((q1 - q0) * n, DN_WPB), (int64_t)h->cus * 4);
+                            hipExtLaunchKernelGGL((k_tile_dn<T, IP, TWD, DN_WPB>), dim3(gd), dim3(DN_WPB * WAVE),
+                                                  0, h->stream, kt.a, kt.b, 0, r0, n, p.tws, p.G, Ap, Aj, Ax, p.B.rows,
+                                                  (const uint32_t*)p.brec, (const int32_t*)p.tptr,
+                                                  (const int64_t*)tile_chunk_items(p, c), cj, cx, alpha,
+                                                  sent(sentinel_region(TWD)), (uint32_t)(q0 * n), (uint32_t)(q1 * n), p.rgs);
+                            return;
+                        }
+                    }
                     hipExtLaunchKernelGGL((k_tile_dn<T, IP, TWD>), dim3(tile_grid(nit, DN_WPB)), dim3(DN_WPB * WAVE),
                                           0, h->stream, kt.a, kt.b, 0, r0, n, p.tws, p.G, Ap, Aj, Ax, p.B.rows,
                                           (const uint32_t*)p.brec, (const int32_t*)p.tptr,

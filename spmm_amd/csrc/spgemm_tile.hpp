@@ -610,6 +610,135 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) __attribute__((amdgpu_waves_per_eu
     }
 }
 
+// k_tile_sym8 with CW waves per task (round 5): the task's bitmap is shared in LDS by the
+// block's waves (the bitmap OR is order-free: ds_or from any wave), each wave walks every CW-th
+// batch of 64 A entries with its own entry table and markers.  The 8 KB bitmap is then paid once
+// per CW waves: 12 KB per 2-wave block instead of 20 KB, so a CU holds 24 waves instead of 16
+// (config 5's symbolic pass was waiting on memory with 4 waves per SIMD).
+struct Sym8Wave {
+    Sym8Ent ent[WAVE];
+    uint8_t mk[TILE_MK];
+};
+template <int CW> struct Sym8Blk {
+    uint32_t bits[SYM8_NW];
+    Sym8Wave w[CW];
+};
+template <typename IP, int CW>
+__global__ __launch_bounds__(CW * WAVE) void k_tile_sym8c(
+    int64_t row0, int64_t nrows, int tws, int G, int twss, const IP* __restrict__ Ap,
+    const int32_t* __restrict__ Aj, const IP* __restrict__ Bp, const uint16_t* __restrict__ Bj16,
+    const uint32_t* __restrict__ sidx, uint32_t* __restrict__ bitmap, int64_t* __restrict__ item_cnt) {
+    constexpr int U = 8;   // chunks of 64 words in flight
+    constexpr int NT = CW * WAVE;
+    __shared__ __attribute__((aligned(16))) Sym8Blk<CW> blk;
+    const int l = lane_id();
+    const int tid = (int)threadIdx.x;
+    const int wv = uniform(tid >> 6);
+    Sym8Wave& S = blk.w[wv];
+    uint32_t* bits = blk.bits;
+    const uint4* __restrict__ W = reinterpret_cast<const uint4*>(Bj16);
+    const int nw = (1 << tws) >> 5;           // bitmap words of a numeric tile
+    const int R = 1 << (twss - tws);          // numeric tiles per symbolic tile
+    const int Gs = (G + R - 1) / R;           // symbolic tiles per row
+    const uint32_t tasks = (uint32_t)(nrows * Gs);
+    for (uint32_t task = xcd_block(gridDim.x); task < tasks; task += gridDim.x) {
+        __syncthreads();   // (the previous task's bitmap has been written out)
+        const int64_t row = row0 + (int64_t)(task / (uint32_t)Gs);
+        const int gs = (int)(task % (uint32_t)Gs);
+        const int t0 = gs * R, t1 = min(G, t0 + R);
+        const int lo16 = (t0 << tws) & 0xffff;
+        const int nws = (t1 - t0) * nw;
+        const int64_t a0 = Ap[row];
+        const int nA = (int)(Ap[row + 1] - a0);
+        if (nA <= 0) {
+            for (int t = t0 + tid; t < t1; t += NT) item_cnt[(row - row0) * G + t] = 0;
+            continue;
+        }
+        for (int w = tid; w < nws; w += NT) bits[w] = 0u;
+        __syncthreads();
+        for (int b = wv * WAVE; b < nA; b += NT) {
+            int wlen = 0;
+            Sym8Ent e{0u, 0u, 0u, 0u};
+            int64_t bg = 0;
+            int cnt = 0;
+            if (b + l < nA) {
+                const int32_t k = Aj[a0 + b + l];
+                const IP rb = Bp[k];
+                if (Gs == 1) {
+                    cnt = (int)(Bp[k + 1] - rb);
+                    bg = (int64_t)rb;
+                } else {
+                    const uint32_t* sk = sidx + (int64_t)k * (Gs + 1);
+                    const uint32_t s0 = sk[gs];
+                    cnt = (int)(sk[gs + 1] - s0);
+                    bg = (int64_t)rb + s0;
+                }
+            }
+            if (cnt > 0) {
+                wlen = (int)(((bg + cnt + 7) >> 3) - (bg >> 3));
+                e.w0 = (uint32_t)(bg >> 3);
+                e.lohi = (uint32_t)(bg & 7) | ((uint32_t)(((bg + cnt - 1) & 7) + 1) << 8);
+            }
+            const int incl = wave_incl_sum_dpp(wlen);
+            const int woff = incl - wlen;
+            const int Wb = readlane_i(incl, WAVE - 1);
+            wsync();
+            e.woff = (uint32_t)woff;
+            e.wlen = (uint32_t)wlen;
+            S.ent[l] = e;
+            wsync();
+            unsigned carry = 0u;
+            for (int gb = 0; gb < Wb; gb += TILE_MK) {
+                group_markers(S, l, wlen, woff, gb);
+                const int nchg = min(TILE_MK, Wb - gb);
+                const uint4 mrow = reinterpret_cast<const uint4*>(S.mk)[l];
+                for (int c0 = 0; c0 < nchg; c0 += U * WAVE) {
+                    const uint64_t mb = marker_bytes(mrow, c0 >> 6);
+                    uint4 w[U];
+                    uint32_t lo[U], hi[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        lo[u] = 8u;   // (no valid column: slots past the group's words)
+                        hi[u] = 0u;
+                        w[u] = make_uint4(0u, 0u, 0u, 0u);
+                        const int cc = c0 + u * WAVE;
+                        if (cc < nchg) {
+                            const unsigned sp = max(wave_incl_umax_dpp((unsigned)(mb >> (8 * u)) & 0xffu), carry);
+                            carry = (unsigned)readlane_i((int)sp, WAVE - 1);
+                            const int t = gb + cc + l;
+                            if (t < Wb) {
+                                const Sym8Ent x = S.ent[(int)sp - 1];
+                                const uint32_t wi = (uint32_t)t - x.woff;
+                                lo[u] = wi == 0u ? (x.lohi & 0xffu) : 0u;
+                                hi[u] = wi + 1u == x.wlen ? (x.lohi >> 8) : 8u;
+                                w[u] = W[x.w0 + wi];
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const uint32_t ww[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
+#pragma unroll
+                        for (int h = 0; h < 8; ++h)
+                            if ((uint32_t)h >= lo[u] && (uint32_t)h < hi[u])
+                                set_bit(bits, (int)((ww[h >> 1] >> (16 * (h & 1))) & 0xffffu) - lo16);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        if (bitmap) {   // (dense numeric tiles take their structure from the accumulation)
+            uint32_t* __restrict__ out = bitmap + ((row - row0) * G + t0) * (int64_t)nw;
+            for (int w = tid; w < nws; w += NT) out[w] = bits[w];
+        }
+        for (int t = tid; t < t1 - t0; t += NT) {
+            int c = 0;
+            for (int j = 0; j < nw; ++j) c += __popc(bits[t * nw + ((j + t) & (nw - 1))]);
+            item_cnt[(row - row0) * G + t0 + t] = c;
+        }
+    }
+}
+
 // Numeric pass of the tile path: one wave per item (row, numeric tile).  Reads the item's
 // bitmap from the symbolic pass, enumerates its products in flattened (jj, kk) order --
 // two adjacent 4-byte loads from tile g's segment table per A entry, one record load per

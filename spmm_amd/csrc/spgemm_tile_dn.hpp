@@ -92,6 +92,9 @@ template <bool NT = (SPG_NT_A != 0), typename R> __device__ __forceinline__ cplx
 constexpr bool SP_NT_A = SPG_NT_A == 2;   // (the sparse-tile kernels)
 
 constexpr int DN_WPB = 2;     // waves per block
+#ifndef SPG_RG_SYNC
+#define SPG_RG_SYNC 1   // items between the barriers of a cooperative record-group block
+#endif
 
 // Per-batch A-entry table: the byte offset of the entry's first product record, shifted by
 // the entry's flattened offset (so product t of the batch reads base[src] + t * RB), and the
@@ -442,13 +445,17 @@ __device__ __forceinline__ void dn_item(DnLds<T, TWD>& S, int l, int TW, int lo,
 // XCD-aware block map (an XCD works through one tile at a time, so the tile's B slice and
 // segment table stay in its L2), the first NB batches' A entries and tile segments loaded up
 // front.
-template <typename T, typename IP, int TWD>
+// RG = 1: the two waves of a block take independent items (tile-major).  RG = DN_WPB (A/B
+// builds, SPG_DN_RGS): the block's two waves take the two tiles of one record group of the same
+// row (items group-major), starting together every SPG_RG_SYNC items, as k_tile_sp<.., RG>.
+template <typename T, typename IP, int TWD, int RG = 1>
 __global__ __launch_bounds__(DN_WPB * WAVE) void k_tile_dn(
     int64_t row0, int64_t nrows, int tws, int G, const IP* __restrict__ Ap,
     const int32_t* __restrict__ Aj, const T* __restrict__ Ax, int64_t K,
     const uint32_t* __restrict__ brec, const int32_t* __restrict__ tptr,
     const int64_t* __restrict__ item_off, int32_t* __restrict__ Cj, T* __restrict__ Cx, T alpha, uint32_t sent,
     uint32_t it_lo, uint32_t it_hi, int rgs) {
+    static_assert(RG == 1 || RG == DN_WPB, "a record group is the block's waves");
     static_assert(OrderedLdsAdd<T>::value || std::is_same<T, float>::value, "ordered LDS add or fp32 runs");
     constexpr int NB = sizeof(T) > 8 ? 4 : 8;    // A batches preloaded per item
     __shared__ __attribute__((aligned(16))) DnLds<T, TWD> lds[DN_WPB];
@@ -457,10 +464,19 @@ __global__ __launch_bounds__(DN_WPB * WAVE) void k_tile_dn(
     DnLds<T, TWD>& S = lds[wv];
     const int TW = 1 << tws;
     const char* __restrict__ rb = reinterpret_cast<const char*>(brec);
-    // items [it_lo, it_hi) (tile-major: a range of whole tiles; rows*G < 2^31 on the host)
-    for (uint32_t it = it_lo + xcd_block(gridDim.x) * DN_WPB + wv; it < it_hi; it += gridDim.x * DN_WPB) {
-        const int g = (int)(it / (uint32_t)nrows);
-        const int64_t row = row0 + (int64_t)(it - (uint32_t)g * (uint32_t)nrows);
+    // items [it_lo, it_hi) (tile-major: a range of whole tiles; rows*G < 2^31 on the host;
+    // RG > 1: (record group, row) items, one per block)
+    constexpr uint32_t PER = RG > 1 ? 1u : (uint32_t)DN_WPB;
+    uint32_t sweep = 0;
+    for (uint32_t it = it_lo + xcd_block(gridDim.x) * PER + (RG > 1 ? 0u : (uint32_t)wv); it < it_hi;
+         it += gridDim.x * PER, ++sweep) {
+        if constexpr (RG > 1) {
+            if (sweep % SPG_RG_SYNC == 0) __syncthreads();
+        }
+        const int grp = (int)(it / (uint32_t)nrows);
+        const int64_t row = row0 + (int64_t)(it - (uint32_t)grp * (uint32_t)nrows);
+        const int g = RG > 1 ? grp * RG + wv : grp;
+        if (RG > 1 && g >= G) continue;   // (a padding tile of the last group)
         const int64_t item = (row - row0) * G + g;
         const int64_t obase = ld_a(item_off + item);
         const int nnz = (int)(ld_a(item_off + item + 1) - obase);
@@ -558,8 +574,13 @@ void k_tile_sp(
     const char* __restrict__ rb = reinterpret_cast<const char*>(brec);
     const bool one = alpha == (T)1;
     // one item per block and sweep (RG == 1: a one-wave block's; RG > 1: the group's RG tiles of a row)
-    for (uint32_t it = it_lo + xcd_block(gridDim.x); it < it_hi; it += gridDim.x) {
-        if constexpr (RG > 1) __syncthreads();    // the block's waves start every item together
+    uint32_t sweep = 0;
+    for (uint32_t it = it_lo + xcd_block(gridDim.x); it < it_hi; it += gridDim.x, ++sweep) {
+        // RG > 1: the block's waves start together every SPG_RG_SYNC items (a persistent grid:
+        // between two barriers a wave that finishes early starts its next item)
+        if constexpr (RG > 1) {
+            if (sweep % SPG_RG_SYNC == 0) __syncthreads();
+        }
         const int grp = (int)(it / (uint32_t)nrows);
         const int64_t row = row0 + (int64_t)(it - (uint32_t)grp * (uint32_t)nrows);
         const int g = RG == 1 ? grp : grp * RG + wv;
