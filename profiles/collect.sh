@@ -26,4 +26,7 @@ timeout -s KILL 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv
     -- python3 bench.py $ARGS --steps 3 --warmup 1 --cpu-seconds 0 > "$P/hit.log" 2>&1
 python3 profiles/summarize.py "$P" > "$OUT/summary_$TAG.txt"
 python3 profiles/pmc_to_json.py "$P" "$PMC_KEY" "$PMC_KERNEL" "$OUT/pmc_traffic.json"
+python3 profiles/kernel_traffic.py "$P" > "$OUT/traffic_$TAG.txt" 2>/dev/null || true
+# (per-dispatch traces are large; the summaries above keep what is used)
+find "$P" -name "*kernel_trace.csv" -delete
 echo "collect done ($TAG)"
