@@ -121,13 +121,23 @@ template <typename T> constexpr int rec_bytes() {
     return (SPG_REC10 && std::is_same<T, double>::value) ? 10 : 4 * rec_words<T>();
 }
 
+#ifndef SPG_REC_NT
+#define SPG_REC_NT 0   // (A/B: record gathers with the non-temporal policy, bypassing the CU's L1)
+#endif
+typedef unsigned int spg_u32x3 __attribute__((ext_vector_type(3)));
 template <typename T, typename IP>
 __device__ __forceinline__ void load_rec(const uint32_t* __restrict__ rec, IP i, int& lc, T& v) {
     constexpr int W = rec_words<T>();
     if constexpr (rec_bytes<T>() == 10) {   // fp64, 10-byte records
         const char* p = reinterpret_cast<const char*>(rec) + (uint64_t)((uint32_t)i * 10u);
         const uint32_t sh = (uint32_t)((uintptr_t)p & 2u) * 8u;     // 0 or 16 bits
-const uint3 x = *reinterpret_cast<const uint3*>(p - ((uintptr_t)p & 2u));
+        uint3 x;
+        if constexpr (SPG_REC_NT) {
+            const spg_u32x3 y = __builtin_nontemporal_load(reinterpret_cast<const spg_u32x3*>(p - ((uintptr_t)p & 2u)));
+            x = make_uint3(y.x, y.y, y.z);
+        } else {
+            x = *reinterpret_cast<const uint3*>(p - ((uintptr_t)p & 2u));
+        }
         const uint32_t lo = __builtin_amdgcn_alignbit(x.y, x.x, sh);
         const uint32_t hi = __builtin_amdgcn_alignbit(x.z, x.y, sh);
         v = __hiloint2double((int)hi, (int)lo);
@@ -152,6 +162,29 @@ const uint3 x = *reinterpret_cast<const uint3*>(p - ((uintptr_t)p & 2u));
     } else {                          // complex128
         __builtin_memcpy(&v, q, sizeof(T));
         lc = (int)q[W - 1];
+    }
+}
+
+// Record at BYTE offset `off` from the (uniform) base `rb`: the 32-bit offset reaches the load
+// as its VGPR offset with the base in SGPRs (global_load ... v_off, s[base]), one VGPR per
+// address instead of a 64-bit pair, no 64-bit address arithmetic per product.
+template <typename T>
+__device__ __forceinline__ void load_rec_at(const char* __restrict__ rb, uint32_t off, int& lc, T& v) {
+    if constexpr (rec_bytes<T>() == 10) {
+        const uint32_t sh = (off & 2u) * 8u;   // records start at 0 or 2 modulo 4
+        uint3 x;
+        if constexpr (SPG_REC_NT) {
+            const spg_u32x3 y = __builtin_nontemporal_load(reinterpret_cast<const spg_u32x3*>(rb + (off & ~3u)));
+            x = make_uint3(y.x, y.y, y.z);
+        } else {
+            x = *reinterpret_cast<const uint3*>(rb + (off & ~3u));
+        }
+        const uint32_t lo = __builtin_amdgcn_alignbit(x.y, x.x, sh);
+        const uint32_t hi = __builtin_amdgcn_alignbit(x.z, x.y, sh);
+        v = __hiloint2double((int)hi, (int)lo);
+        lc = (int)((x.z >> sh) & 0xffffu);
+    } else {
+        load_rec(reinterpret_cast<const uint32_t*>(rb + off), 0, lc, v);
     }
 }
 

@@ -275,7 +275,7 @@ __device__ __forceinline__ void dn_walk(L* lp, T* acc, int l, const int32_t* __r
                             qc[u] = (int)(((eb + t * 2654435761u) >> 22) & 1023u);
                             qv[u] = (T)1;
                         } else {
-                            load_rec(reinterpret_cast<const uint32_t*>(rb + (eb + __umul24(t, RB))), 0, qc[u], qv[u]);
+                            load_rec_at(rb, eb + __umul24(t, RB), qc[u], qv[u]);
                         }
                     }
 #pragma unroll
@@ -529,7 +529,10 @@ using SpCfg2048 = SpCfg<2048, 256, WAVE, 16>;   // fp64 8192-column tiles (21.0 
 // SPG_SP_RGS > 0): 20,432 bytes per wave, so two 4-wave blocks (8 waves) fit a CU's 160 KB;
 // 2032 slots per window (config 5's items hold 1887 +- 40 entries) and 8 lane slots (an
 // out-of-window add conflicts at most 8 ways)
-using SpCfgRG = SpCfg<2032, 256, 8, 16>;
+#ifndef SPG_RG_MKB
+#define SPG_RG_MKB 16   // (A/B: chunks per marker group of the cooperative kernel)
+#endif
+using SpCfgRG = SpCfg<2032, 256, 8, SPG_RG_MKB>;
 template <typename T, typename CF> struct SpLds {
     T acc[CF::CAP + CF::DUMMY];         // compact accumulator of one window; + lane slots
     uint2 bw[CF::NW];                   // (bitmap word, popcount prefix)
