@@ -136,7 +136,9 @@ inline size_t vbytes(spg_dtype_t t) {
 }
 
 // bytes of one tile-major B record of the tile path (column in tile + value, unpadded)
-inline size_t brec_bytes(spg_dtype_t t) { return (SPG_REC10 && t == SPG_R_64F) ? 10 : 4 + vbytes(t); }
+inline size_t brec_bytes(spg_dtype_t t) {
+    return (SPG_REC10 && t == SPG_R_64F) ? 10 : (SPG_REC6 && t == SPG_R_32F) ? 6 : 4 + vbytes(t);
+}
 
 // Runs f(T{}) with T the C++ type of value type t.
 // (SPG_ONLY_F64: fp64-only development builds for A/B timing, about 3x faster to compile;
@@ -653,6 +655,9 @@ inline bool fp32_runs(const spg_plan_s& p) {
 // 19.1 ms for independent items, round 5)
 #ifndef SPG_DN_RGS
 #define SPG_DN_RGS 0
+#endif
+#ifndef SPG_DN_RG_PERSIST
+#define SPG_DN_RG_PERSIST 1
 #endif
 inline int record_group_log2(const spg_plan_s& p) {
     if (SPG_DN_RGS > 0 && p.use_tile && tile_dense(p) && p.lean && p.A.value_type == SPG_R_64F && p.tws == 11)
@@ -1176,7 +1181,8 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
                     if constexpr (SPG_DN_RGS > 0 && TWD == 2048) {
                         if (p.rgs == SPG_DN_RGS) {   // record groups of DN_WPB tiles, one per block
                             const int64_t q0 = g0 >> p.rgs, q1 = (g1 + DN_WPB - 1) >> p.rgs;
-                            const unsigned gd = (unsigned)std::min<int64_t>(coop_grid((q1 - q0) * n, DN_WPB), (int64_t)h->cus * 4);
+                            const unsigned gd = (unsigned)std::min<int64_t>(coop_grid((q1 - q0) * n, DN_WPB),
+                                                                            SPG_DN_RG_PERSIST ? (int64_t)h->cus * 4 : ((int64_t)1 << 30));
                             hipExtLaunchKernelGGL((k_tile_dn<T, IP, TWD, DN_WPB>), dim3(gd), dim3(DN_WPB * WAVE),
                                                   0, h->stream, kt.a, kt.b, 0, r0, n, p.tws, p.G, Ap, Aj, Ax, p.B.rows,
                                                   (const uint32_t*)p.brec, (const int32_t*)p.tptr,

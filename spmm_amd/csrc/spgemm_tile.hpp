@@ -117,8 +117,16 @@ template <typename T> constexpr int rec_words() { return 1 + (int)(sizeof(T) / 4
 #ifndef SPG_REC10
 #define SPG_REC10 1
 #endif
+// SPG_REC6 (round 5, default): fp32 records of 6 bytes the same way -- the value, then the column
+// inside the tile as u16 (fp32 tiles are at most 4096 columns wide) -- record i at byte 6i (0 or 2
+// modulo 4): one dwordx2 from the dword below it, one v_alignbit.  8 -> 6 bytes per product of
+// gather traffic for the fp32 tile kernels.
+#ifndef SPG_REC6
+#define SPG_REC6 1
+#endif
 template <typename T> constexpr int rec_bytes() {
-    return (SPG_REC10 && std::is_same<T, double>::value) ? 10 : 4 * rec_words<T>();
+    return (SPG_REC10 && std::is_same<T, double>::value) ? 10
+           : (SPG_REC6 && std::is_same<T, float>::value) ? 6 : 4 * rec_words<T>();
 }
 
 #ifndef SPG_REC_NT
@@ -142,6 +150,13 @@ __device__ __forceinline__ void load_rec(const uint32_t* __restrict__ rec, IP i,
         const uint32_t hi = __builtin_amdgcn_alignbit(x.z, x.y, sh);
         v = __hiloint2double((int)hi, (int)lo);
         lc = (int)((x.z >> sh) & 0xffffu);
+        return;
+    } else if constexpr (rec_bytes<T>() == 6) {   // fp32, 6-byte records
+        const char* p = reinterpret_cast<const char*>(rec) + (uint64_t)((uint32_t)i * 6u);
+        const uint32_t sh = (uint32_t)((uintptr_t)p & 2u) * 8u;
+        const uint2 x = *reinterpret_cast<const uint2*>(p - ((uintptr_t)p & 2u));
+        v = __uint_as_float(__builtin_amdgcn_alignbit(x.y, x.x, sh));
+        lc = (int)((x.y >> sh) & 0xffffu);
         return;
     }
     const uint32_t* __restrict__ q =
@@ -183,6 +198,11 @@ __device__ __forceinline__ void load_rec_at(const char* __restrict__ rb, uint32_
         const uint32_t hi = __builtin_amdgcn_alignbit(x.z, x.y, sh);
         v = __hiloint2double((int)hi, (int)lo);
         lc = (int)((x.z >> sh) & 0xffffu);
+    } else if constexpr (rec_bytes<T>() == 6) {
+        const uint32_t sh = (off & 2u) * 8u;
+        const uint2 x = *reinterpret_cast<const uint2*>(rb + (off & ~3u));
+        v = __uint_as_float(__builtin_amdgcn_alignbit(x.y, x.x, sh));
+        lc = (int)((x.y >> sh) & 0xffffu);
     } else {
         load_rec(reinterpret_cast<const uint32_t*>(rb + off), 0, lc, v);
     }
@@ -190,6 +210,14 @@ __device__ __forceinline__ void load_rec_at(const char* __restrict__ rb, uint32_
 
 template <typename T>
 __device__ __forceinline__ void store_rec(uint32_t* __restrict__ rec, int64_t i, int lc, T v) {
+    if constexpr (rec_bytes<T>() == 6) {   // three 2-byte stores
+        uint16_t* q = reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(rec) + i * 6);
+        const uint32_t b = __float_as_uint(v);
+        q[0] = (uint16_t)b;
+        q[1] = (uint16_t)(b >> 16);
+        q[2] = (uint16_t)lc;
+        return;
+    }
     if constexpr (rec_bytes<T>() == 10) {   // five 2-byte stores (a record is 2-byte aligned)
         uint16_t* q = reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(rec) + i * 10);
         uint64_t b;
@@ -209,7 +237,9 @@ __device__ __forceinline__ void store_rec(uint32_t* __restrict__ rec, int64_t i,
 // structure first, values group by group as they arrive).
 template <typename T>
 __device__ __forceinline__ void store_rec_col(uint32_t* __restrict__ rec, int64_t i, int lc) {
-    if constexpr (rec_bytes<T>() == 10) {
+    if constexpr (rec_bytes<T>() == 6) {
+        reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(rec) + i * 6)[2] = (uint16_t)lc;
+    } else if constexpr (rec_bytes<T>() == 10) {
         reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(rec) + i * 10)[4] = (uint16_t)lc;
     } else {
         rec[i * rec_words<T>() + rec_words<T>() - 1] = (uint32_t)lc;
@@ -217,7 +247,12 @@ __device__ __forceinline__ void store_rec_col(uint32_t* __restrict__ rec, int64_
 }
 template <typename T>
 __device__ __forceinline__ void store_rec_val(uint32_t* __restrict__ rec, int64_t i, T v) {
-    if constexpr (rec_bytes<T>() == 10) {
+    if constexpr (rec_bytes<T>() == 6) {
+        uint16_t* q = reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(rec) + i * 6);
+        const uint32_t b = __float_as_uint(v);
+        q[0] = (uint16_t)b;
+        q[1] = (uint16_t)(b >> 16);
+    } else if constexpr (rec_bytes<T>() == 10) {
         uint16_t* q = reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(rec) + i * 10);
         uint64_t b;
         __builtin_memcpy(&b, &v, 8);
