@@ -481,9 +481,12 @@ def broadcast_ms(ctx, B):
 
 def pipeline_report(ctx, args, A, B, alg, cf, hook, ms):
     """How much of B's values broadcast the step hides (N > 1): the values broadcast alone
-    (median of 3), the step with the values in one broadcast that overlaps only the
-    symbolic pass (2 steps), and the step as measured.  hidden_ms = unpipelined - measured;
-    overlap_frac = hidden_ms / values_broadcast_ms.  None on the CPU test path."""
+    and B's structure broadcast alone (median of 3 each; the structure is what every
+    rank waits for before its layout and symbolic pass), the step with the values in one
+    broadcast that overlaps only the symbolic pass (2 steps), and the step as measured
+    (tile-major value groups in flight from before the symbolic pass through the numeric
+    tiles).  hidden_ms = unpipelined - measured; overlap_frac = hidden_ms /
+    values_broadcast_ms.  None on the CPU test path."""
     if not ctx.gpu or hook is not None:
         return None
     from spmm_amd import distributed
@@ -504,6 +507,16 @@ def pipeline_report(ctx, args, A, B, alg, cf, hook, ms):
         ctx.barrier()
         ts.append(time.perf_counter() - t0)
     vms = float(np.median(ts)) * 1e3
+    ts = []
+    for _ in range(3):
+        ctx.sync()
+        ctx.barrier()
+        t0 = time.perf_counter()
+        distributed.broadcast_csr(B, 0, ctx.dev, values=False)
+        ctx.sync()
+        ctx.barrier()
+        ts.append(time.perf_counter() - t0)
+    sms = float(np.median(ts)) * 1e3
     pipelined = not args.no_pipeline
     last = distributed.rowblock_step.last
 
@@ -518,7 +531,8 @@ def pipeline_report(ctx, args, A, B, alg, cf, hook, ms):
     ums, pms = (oms, ms) if pipelined else (ms, oms)
     groups = len(last.groups) if (pipelined and last is not None and last.pipelined) else None
     return {"pipelined": pipelined and groups is not None, "groups": groups,
-            "values_broadcast_ms": round(vms, 3), "step_ms_unpipelined": round(ums, 4),
+            "values_broadcast_ms": round(vms, 3), "structure_broadcast_ms": round(sms, 3),
+            "step_ms_unpipelined": round(ums, 4),
             "step_ms_pipelined": round(pms, 4), "hidden_ms": round(ums - pms, 4),
             "overlap_frac": round((ums - pms) / vms, 4) if vms > 0 else None}
 

@@ -267,7 +267,9 @@ spg_status_t spg_spgemm_ws(spg_handle_t handle, const spg_csr_t *A, const spg_cs
  *     values in TILE-MAJOR order -- B's entries with columns in value tile 0 row by row,
  *     then value tile 1, ...  One device->host copy.  The order depends only on B's
  *     structure and the value-tile width, so plans on different devices with equal widths
- *     agree.
+ *     agree.  Valid right after spg_plan: the first of these calls (or spg_symbolic) builds
+ *     the plan's tile layout from B's structure, so the values can be sent while the
+ *     symbolic pass runs.
  *   spg_tile_values: B's values (row-major, B->values of the plan) permuted into that
  *     order (nnz(B) entries of B's value type) -- on the device that holds them.
  *   spg_numeric_tiles: C's entries in columns of value tiles [tile_begin, tile_end) from the

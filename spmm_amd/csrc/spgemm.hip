@@ -1830,21 +1830,25 @@ spg_status_t spg_numeric(spg_handle_t h, spg_plan_t p, const void* alpha, spg_cs
 }
 
 // ---- the numeric phase by column-tile groups (include/spgemm.h; multi-GPU B-value pipelining)
-static spg_status_t tiles_supported(spg_plan_t p) {
+// The segment tables are built by spg_symbolic, or here on first use: a plan's values can
+// be laid out tile-major (and their offsets read) before its symbolic pass, so the multi-GPU
+// step sends them while the symbolic pass runs.  (Call under the handle's DeviceGuard.)
+static spg_status_t tiles_supported(spg_handle_t h, spg_plan_t p) {
     if (!p) return SPG_STATUS_INVALID_VALUE;
     if (!p->use_tile || tile_chunks(*p) != 1 || p->alg1_fused) return SPG_STATUS_NOT_SUPPORTED;
-    if (!p->tidx_built) return SPG_STATUS_NOT_INITIALIZED;   // spg_symbolic builds the table
-    return SPG_STATUS_SUCCESS;
+    if (p->tidx_built) return SPG_STATUS_SUCCESS;
+    return p->A.indptr_type == SPG_INDEX_64I ? tile_build_index<int64_t>(h, *p) : tile_build_index<int32_t>(h, *p);
 }
 
 spg_status_t spg_tile_value_offsets(spg_handle_t h, spg_plan_t p, int64_t* offsets, int64_t capacity) {
     if (!h) return SPG_STATUS_NOT_INITIALIZED;
-    spg_status_t st = tiles_supported(p);
+    if (!p) return SPG_STATUS_INVALID_VALUE;
+    DeviceGuard dg_(h->device);
+    SPG_HIP(h, dg_.err);
+    spg_status_t st = tiles_supported(h, p);
     if (st) return st;
     const int64_t Gq = rec_groups(*p);   // value tiles = record groups
     if (capacity < Gq + 1 || !offsets) return SPG_STATUS_INVALID_VALUE;
-    DeviceGuard dg_(h->device);
-    SPG_HIP(h, dg_.err);
     // group q starts at table word q*W; the last group's end slot holds nnz(B)
     const int64_t W = group_words(*p);
     std::vector<int32_t> w((size_t)Gq + 1);
@@ -1859,13 +1863,14 @@ spg_status_t spg_tile_value_offsets(spg_handle_t h, spg_plan_t p, int64_t* offse
 
 spg_status_t spg_tile_values(spg_handle_t h, spg_plan_t p, void* tm) {
     if (!h) return SPG_STATUS_NOT_INITIALIZED;
-    spg_status_t st = tiles_supported(p);
+    if (!p) return SPG_STATUS_INVALID_VALUE;
+    DeviceGuard dg_(h->device);
+    SPG_HIP(h, dg_.err);
+    spg_status_t st = tiles_supported(h, p);
     if (st) return st;
     if (!tm && p->B.nnz > 0) return SPG_STATUS_INVALID_VALUE;
     if (p->B.nnz > 0 && !p->B.values) return SPG_STATUS_INVALID_VALUE;
     if (p->B.rows == 0 || p->B.nnz == 0) return SPG_STATUS_SUCCESS;
-    DeviceGuard dg_(h->device);
-    SPG_HIP(h, dg_.err);
     const bool i64 = p->A.indptr_type == SPG_INDEX_64I;
     return dispatch_value(p->A.value_type, [&](auto tag) {
         using T = decltype(tag);
@@ -1886,7 +1891,9 @@ spg_status_t spg_numeric_tiles(spg_handle_t h, spg_plan_t p, const void* alpha, 
     if (!h) return SPG_STATUS_NOT_INITIALIZED;
     if (!p || !alpha || !C) return SPG_STATUS_INVALID_VALUE;
     if (p->nnzC < 0) return SPG_STATUS_NOT_INITIALIZED;     // spg_symbolic first
-    spg_status_t st = tiles_supported(p);
+    DeviceGuard dg_(h->device);
+    SPG_HIP(h, dg_.err);
+    spg_status_t st = tiles_supported(h, p);   // (spg_symbolic built the tables)
     if (st) return st;
     if (g0 < 0 || g1 > rec_groups(*p) || g0 > g1) return SPG_STATUS_INVALID_VALUE;   // value tiles
     if (C->rows != p->A.rows || C->cols != p->B.cols) return SPG_STATUS_INVALID_VALUE;
@@ -1896,8 +1903,6 @@ spg_status_t spg_numeric_tiles(spg_handle_t h, spg_plan_t p, const void* alpha, 
     if (p->nnzC > 0 && (!C->indices || !C->values)) return SPG_STATUS_INVALID_VALUE;
     if (p->B.nnz > 0 && !tm) return SPG_STATUS_INVALID_VALUE;
     if (p->nnzC == 0 || g0 == g1) return SPG_STATUS_SUCCESS;
-    DeviceGuard dg_(h->device);
-    SPG_HIP(h, dg_.err);
     const bool i64 = p->A.indptr_type == SPG_INDEX_64I;
     return dispatch_value(p->A.value_type, [&](auto tag) {
         using T = decltype(tag);

@@ -137,7 +137,9 @@ def _spgemm(a, b, alpha=1, alg=0, chunk_fraction=0.2, verbose=False, before_nume
     are queued together).
 
     `by_tiles(geom)`: the numeric pass by column-tile groups (spg_numeric_tiles), called
-    exactly once per product, after the symbolic pass.  `geom` is None when the plan cannot
+    exactly once per product, BEFORE the symbolic pass (the plan's tile layout needs only
+    B's structure, so B's values can travel while the symbolic pass runs; _spgemm_by_tiles).
+    `geom` is None when the plan cannot
     run by tiles (not the tile path, several row chunks, ALG1); then `by_tiles` makes
     b.data complete and returns None, and spg_numeric runs.  Otherwise geom is a dict
     (tile_width, tiles, offsets: the tiles + 1 tile-major value offsets, tile_values(): B's
@@ -180,6 +182,8 @@ def _spgemm(a, b, alpha=1, alg=0, chunk_fraction=0.2, verbose=False, before_nume
         if by_tiles(None) is not None:
             raise RuntimeError("by_tiles must complete B's values when geom is None")
         by_tiles = None
+    if by_tiles is not None:
+        return _spgemm_by_tiles(h, a, b, alpha, algo, cf, by_tiles, verbose)
     if fp is not None:   # the same sequence in one native call (csrc/fastpath.cpp)
         al = complex(alpha)
         st, data, indices, indptr, wsb, peak = fp.spgemm(
@@ -233,10 +237,7 @@ def _spgemm(a, b, alpha=1, alg=0, chunk_fraction=0.2, verbose=False, before_nume
                         data.data_ptr() if nnzc else 0, _IT[indptr.dtype], _VT[data.dtype])
             if before_numeric is not None:
                 before_numeric()
-            if by_tiles is not None and _numeric_by_tiles(h, plan, b, al, vc, by_tiles):
-                pass
-            else:
-                check(lib.spg_numeric(h.ptr, plan, ctypes.byref(al), ctypes.byref(vc)), "spg_numeric")
+            check(lib.spg_numeric(h.ptr, plan, ctypes.byref(al), ctypes.byref(vc)), "spg_numeric")
         finally:
             lib.spg_plan_destroy(plan)
     if wide and nnzc < 2 ** 31:
@@ -246,47 +247,104 @@ def _spgemm(a, b, alpha=1, alg=0, chunk_fraction=0.2, verbose=False, before_nume
     return csr_matrix._from_parts(data, indices, indptr, (m, n), canonical=True)
 
 
-def _numeric_by_tiles(h, plan, b, al, vc, by_tiles) -> bool:
-    """The numeric pass through spg_numeric_tiles, group by group as `by_tiles` releases
-    them (see _spgemm).  False when `by_tiles` took the spg_numeric fallback."""
+def _alpha_of(dtype, alpha):
+    ct, nparts = _ALPHA_CT[dtype]
+    return (ct * 2)(complex(alpha).real, complex(alpha).imag) if nparts == 2 else ct(float(alpha))
+
+
+def _spgemm_by_tiles(h, a, b, alpha, algo, cf, by_tiles, verbose):
+    """_spgemm with `by_tiles` (the row-block step of spmm_amd.distributed): spg_plan, then
+    the tile geometry -- spg_tile_value_offsets builds the plan's tile layout from B's
+    structure alone -- and ``by_tiles(geom)``, which starts B's values travelling group by
+    group; only then spg_symbolic, which runs while they arrive, and the numeric tiles of
+    each group as it is released (spg_numeric after the row-major fallback)."""
+    lib = h.lib
+    m, n = a.shape[0], b.shape[1]
+    dev = a.device
+    va, vb = _csr_view(a), _csr_view(b)
+    ws_bytes = ctypes.c_size_t(0)
+    check(lib.spg_plan(h.ptr, ctypes.byref(va), ctypes.byref(vb), algo, cf, ctypes.byref(ws_bytes), None, None),
+          "spg_plan")
+    if verbose:
+        print("USING ALG", algo, "workspace GB =", ws_bytes.value / (1024 ** 3))
+    ws = torch.empty(max(ws_bytes.value, 1), dtype=torch.uint8, device=dev)
+    plan = ctypes.c_void_p()
+    check(lib.spg_plan(h.ptr, ctypes.byref(va), ctypes.byref(vb), algo, cf, ctypes.byref(ws_bytes),
+                       ctypes.c_void_p(ws.data_ptr()), ctypes.byref(plan)), "spg_plan")
+    al = _alpha_of(a.data.dtype, alpha)
+    try:
+        geom = _tile_geometry(h, plan, b)
+        got = by_tiles(geom)
+        if got is not None and geom is None:
+            raise RuntimeError("by_tiles returned tile groups for a plan that cannot run by tiles")
+        nnz = ctypes.c_int64(0)
+        wide = a.nnz * (b.nnz / max(b.shape[0], 1)) >= 2 ** 31
+        for it in ((torch.int64,) if wide else (torch.int32, torch.int64)):
+            indptr = torch.empty(m + 1, dtype=it, device=dev)
+            st = lib.spg_symbolic(h.ptr, plan, ctypes.c_void_p(indptr.data_ptr()), _IT[it], ctypes.byref(nnz))
+            if st != _lib.STATUS_OVERFLOW:
+                break
+        check(st, "spg_symbolic")
+        nnzc = int(nnz.value)
+        indices = torch.empty(nnzc, dtype=torch.int32, device=dev)
+        data = torch.empty(nnzc, dtype=a.data.dtype, device=dev)
+        vc = SpgCsr(m, n, nnzc, indptr.data_ptr(), indices.data_ptr() if nnzc else 0,
+                    data.data_ptr() if nnzc else 0, _IT[indptr.dtype], _VT[data.dtype])
+        if got is None:
+            check(lib.spg_numeric(h.ptr, plan, ctypes.byref(al), ctypes.byref(vc)), "spg_numeric")
+        else:
+            _numeric_groups(h, plan, al, vc, got, geom)
+        peak = ctypes.c_size_t(0)
+        check(lib.spg_peak_bytes(plan, ctypes.byref(peak)), "spg_peak_bytes")
+    finally:
+        lib.spg_plan_destroy(plan)
+    if wide and nnzc < 2 ** 31:
+        indptr = indptr.to(torch.int32)   # the int32 contract when the result fits
+    last_stats.alg, last_stats.workspace_bytes = int(algo), int(ws_bytes.value)
+    last_stats.peak_bytes, last_stats.nnz = int(peak.value), nnzc
+    return csr_matrix._from_parts(data, indices, indptr, (m, n), canonical=True)
+
+
+def _tile_geometry(h, plan, b):
+    """The by_tiles geometry of a plan (see _spgemm), or None when it cannot run by tiles."""
     lib = h.lib
     info = _lib.SpgPlanInfo()
     check(lib.spg_plan_info(plan, ctypes.byref(info), None, 0), "spg_plan_info")
-    geom = None
     # (a development library built without the tile-group entry points: spg_numeric)
     has_tiles = all(hasattr(lib, f) for f in ("spg_tile_value_offsets", "spg_tile_values", "spg_numeric_tiles"))
-    if has_tiles and info.path == 2 and info.n_chunks == 1:
-        # value tiles: record_group adjacent numeric tiles (include/spgemm.h)
-        rg = max(1, int(info.record_group))
-        G = (int(info.tiles_per_row) + rg - 1) // rg
-        offs = (ctypes.c_int64 * (G + 1))()
-        st = lib.spg_tile_value_offsets(h.ptr, plan, offs, G + 1)
-        if st == 0:
-            def tile_values():
-                tm = torch.empty(max(b.nnz, 1), dtype=b.data.dtype, device=b.data.device)
-                check(lib.spg_tile_values(h.ptr, plan, ctypes.c_void_p(tm.data_ptr())), "spg_tile_values")
-                return tm[:b.nnz]
-            geom = {"tile_width": int(info.tile_width) * rg, "tiles": G, "offsets": np.frombuffer(offs, dtype=np.int64).copy(),
-                    "tile_values": tile_values, "dtype": b.data.dtype}
-        elif st != _lib.STATUS_NOT_SUPPORTED:
-            check(st, "spg_tile_value_offsets")
-    got = by_tiles(geom)
-    if got is None:
-        return False
-    if geom is None:
-        raise RuntimeError("by_tiles returned tile groups for a plan that cannot run by tiles")
+    if not (has_tiles and info.path == 2 and info.n_chunks == 1):
+        return None
+    # value tiles: record_group adjacent numeric tiles (include/spgemm.h)
+    rg = max(1, int(info.record_group))
+    G = (int(info.tiles_per_row) + rg - 1) // rg
+    offs = (ctypes.c_int64 * (G + 1))()
+    st = lib.spg_tile_value_offsets(h.ptr, plan, offs, G + 1)
+    if st == _lib.STATUS_NOT_SUPPORTED:
+        return None
+    check(st, "spg_tile_value_offsets")
+
+    def tile_values():
+        tm = torch.empty(max(b.nnz, 1), dtype=b.data.dtype, device=b.data.device)
+        check(lib.spg_tile_values(h.ptr, plan, ctypes.c_void_p(tm.data_ptr())), "spg_tile_values")
+        return tm[:b.nnz]
+    return {"tile_width": int(info.tile_width) * rg, "tiles": G,
+            "offsets": np.frombuffer(offs, dtype=np.int64).copy(), "tile_values": tile_values,
+            "dtype": b.data.dtype}
+
+
+def _numeric_groups(h, plan, al, vc, got, geom):
+    """spg_numeric_tiles for each (tile_begin, tile_end) group `by_tiles` releases."""
     tm, groups = got
     covered = 0
     for g0, g1 in groups:
         if g0 != covered:
             raise RuntimeError(f"tile groups must be consecutive: expected {covered}, got {g0}")
-        check(lib.spg_numeric_tiles(h.ptr, plan, ctypes.byref(al), ctypes.byref(vc),
-                                    ctypes.c_void_p(tm.data_ptr() if tm.numel() else 0), int(g0), int(g1)),
+        check(h.lib.spg_numeric_tiles(h.ptr, plan, ctypes.byref(al), ctypes.byref(vc),
+                                      ctypes.c_void_p(tm.data_ptr() if tm.numel() else 0), int(g0), int(g1)),
               "spg_numeric_tiles")
         covered = g1
     if covered != geom["tiles"]:
         raise RuntimeError(f"tile groups covered {covered} of {geom['tiles']} tiles")
-    return True
 
 
 def spmv(a, x, y=None, alpha=1, beta=0, transa=False):

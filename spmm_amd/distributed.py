@@ -13,14 +13,15 @@ cross-GPU reduction.  The collectives are
   torch.distributed.  With ``async_values=True`` the values broadcast is left in flight and
   its work handle returned, so the symbolic pass (which reads only B's structure) runs
   while the values arrive (``spgemm_rowblock``'s ``before_numeric`` waits for them);
-* ``broadcast_tile_values`` (``rowblock_step(..., pipeline=True)``, the default on GPUs):
-  B's structure as above, then the symbolic pass, then B's values in TILE-MAJOR order
-  (spg_tile_values on ``src``: the entries of column tile 0 row by row, then tile 1, ...)
-  as one async broadcast per group of column tiles; each group's numeric tiles
-  (spg_numeric_tiles) start when its slice lands, so the values broadcast overlaps the
-  numeric pass, not only the symbolic pass.  The ranks first agree (one 3-int64
-  all_gather) that every plan runs by tiles with the same tile width; otherwise the step
-  falls back to the row-major values broadcast and spg_numeric;
+* ``TileValueBroadcast`` (``rowblock_step(..., pipeline=True)``, the default on GPUs):
+  B's structure as above; each rank plans and lays out its tiles from the structure alone
+  (spg_tile_value_offsets); then B's values go out in TILE-MAJOR order (spg_tile_values on
+  ``src``: the entries of column tile 0 row by row, then tile 1, ...) as one async
+  broadcast per group of column tiles, BEFORE the symbolic pass, which runs while they
+  travel; each group's numeric tiles (spg_numeric_tiles) start when its slice lands, so
+  the values broadcast overlaps the symbolic pass and the numeric pass.  The ranks first
+  agree (one 4-int64 all_gather) that every plan runs by tiles with the same tile width;
+  otherwise the step falls back to the row-major values broadcast and spg_numeric;
 * ``allgather_nnz``: every rank's nnz(C slab) -> global row-pointer offsets, when a
   stitched C is wanted.
 
@@ -282,7 +283,8 @@ def rowblock_step(A_block: csr_matrix, B_src: csr_matrix | None, src: int, devic
                   chunk_fraction: float = 0.2, multiply=None, group=None, pipeline: bool | None = None,
                   n_groups: int = 8):
     """One C = A.B step of the row-block scheme on this rank: B arrives from `src` (its
-    structure first; the values stay in flight through the symbolic pass), then this
+    structure first; the values stay in flight through the symbolic pass and, pipelined,
+    the numeric tiles), then this
     rank's slab A_block . B.  `multiply(A_block, B, wait_values)` replaces the device
     multiply (the gloo tests run the CPU oracle there).  `pipeline` (default: on a GPU
     device): the values travel tile-major in `n_groups` async broadcasts, each group's
