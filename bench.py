@@ -517,6 +517,10 @@ def pipeline_report(ctx, args, A, B, alg, cf, hook, ms):
         ctx.barrier()
         ts.append(time.perf_counter() - t0)
     sms = float(np.median(ts)) * 1e3
+    sbytes = None
+    if B is not None:   # (rank 0 prints the line)
+        nb1 = distributed.cols16_layout(B.shape[0], B.shape[1], B.nnz)
+        sbytes = B.indptr.element_size() * (B.shape[0] + 1) + (4 * B.nnz if nb1 < 0 else 4 * B.shape[0] * nb1 + 2 * B.nnz)
     pipelined = not args.no_pipeline
     last = distributed.rowblock_step.last
 
@@ -532,6 +536,7 @@ def pipeline_report(ctx, args, A, B, alg, cf, hook, ms):
     groups = len(last.groups) if (pipelined and last is not None and last.pipelined) else None
     return {"pipelined": pipelined and groups is not None, "groups": groups,
             "values_broadcast_ms": round(vms, 3), "structure_broadcast_ms": round(sms, 3),
+            "structure_bytes": sbytes, "values_bytes": nnzB * esz,
             "step_ms_unpipelined": round(ums, 4),
             "step_ms_pipelined": round(pms, 4), "hidden_ms": round(ums - pms, 4),
             "overlap_frac": round((ums - pms) / vms, 4) if vms > 0 else None}

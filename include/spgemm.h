@@ -281,6 +281,20 @@ spg_status_t spg_tile_values(spg_handle_t handle, spg_plan_t plan, void *tile_ma
 spg_status_t spg_numeric_tiles(spg_handle_t handle, spg_plan_t plan, const void *alpha, spg_csr_t *C,
                                const void *tile_major_values, int64_t tile_begin, int64_t tile_end);
 
+/* B's column indices in 16 bits, for the multi-GPU structure broadcast (spmm_amd.
+ * distributed.broadcast_csr; no cuSPARSE counterpart -- the reference broadcasts B's int32
+ * indices as they are, modify_src/cupy-src/cupyx/distributed/_nccl_comm.py:651-674).  The
+ * columns of M are cut into blocks of 65536; per row, the ceil(cols / 65536) - 1 interior
+ * block starts (the offset from the row's start of its first entry with column >= c * 65536,
+ * or the row's length, for c = 1, 2, ...; uint32, row-major) plus the low 16 bits of every
+ * column carry the indices exactly, in 2 bytes per entry + 4 per row and interior block
+ * (config 5's B: 141 MB instead of 276 MB).  M canonical (rows sorted); stream-ordered.
+ *   spg_cols16_split: M's indptr/indices -> block_starts, lo16 (nnz entries).  block_starts
+ *     may be NULL for M at most 65536 columns wide.  M->values is not read.
+ *   spg_cols16_join: block_starts, lo16 and M's indptr -> M->indices. */
+spg_status_t spg_cols16_split(spg_handle_t handle, const spg_csr_t *M, uint32_t *block_starts, uint16_t *lo16);
+spg_status_t spg_cols16_join(spg_handle_t handle, spg_csr_t *M, const uint32_t *block_starts, const uint16_t *lo16);
+
 /* Per-phase device timing: with timing enabled every kernel the handle launches is
  * bracketed by hipEvents on the handle's stream, and spg_get_timing returns the
  * accumulated device milliseconds and launch counts per phase (the build's equivalent of

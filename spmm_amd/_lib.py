@@ -46,7 +46,7 @@ EXPORTS = ("spg_version", "spg_build_info", "spg_status_string", "spg_create", "
            "spg_numeric", "spg_peak_bytes", "spg_validate_csr", "spg_plan_destroy",
            "spg_set_timing", "spg_get_timing", "spg_result_in_workspace", "spg_spmv",
            "spg_spgemm_ws", "spg_plan_info", "spg_tile_value_offsets", "spg_tile_values",
-           "spg_numeric_tiles")
+           "spg_numeric_tiles", "spg_cols16_split", "spg_cols16_join")
 
 PHASES = ("products", "scan", "symbolic", "numeric", "compact", "validate", "spill", "spmv", "b_layout")
 NUM_PHASES = 9
@@ -125,6 +125,8 @@ def load():
             "spg_tile_value_offsets": (ctypes.c_int, [vp, vp, ctypes.POINTER(i64), i64]),
             "spg_tile_values": (ctypes.c_int, [vp, vp, vp]),
             "spg_numeric_tiles": (ctypes.c_int, [vp, vp, vp, csrp, vp, i64, i64]),
+            "spg_cols16_split": (ctypes.c_int, [vp, csrp, vp, vp]),
+            "spg_cols16_join": (ctypes.c_int, [vp, csrp, vp, vp]),
             "spg_set_timing": (ctypes.c_int, [vp, ctypes.c_int]),
             "spg_get_timing": (ctypes.c_int, [vp, ctypes.POINTER(SpgTiming)]),
         }

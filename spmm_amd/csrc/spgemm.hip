@@ -1387,6 +1387,54 @@ spg_status_t validate_typed(spg_handle_t h, const spg_csr_t& M, int* flags) {
 }  // namespace
 
 // =============================================================================== C ABI
+// ---- 16-bit columns for the structure broadcast (include/spgemm.h, spg_cols16_*)
+// One wave per row.  Split: every column's low half, and where the row's columns reach each
+// interior block start c * 65536 (the first entry whose high half is >= c; the row length
+// when none is).  Each start is written by exactly one lane: the entry whose high half
+// steps over it, or the tail loop for blocks past the row's last column.
+template <typename IP>
+__global__ __launch_bounds__(256) void k_cols16_split(int64_t rows, const IP* __restrict__ Mp,
+                                                      const int32_t* __restrict__ Mj, int nb1,
+                                                      uint32_t* __restrict__ starts, uint16_t* __restrict__ lo16) {
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const int l = lane_id();
+    const int64_t b = (int64_t)Mp[row];
+    const uint32_t len = (uint32_t)((int64_t)Mp[row + 1] - b);
+    uint32_t* __restrict__ st = starts + row * nb1;
+    for (uint32_t i = l; i < len; i += WAVE) {
+        const uint32_t c = (uint32_t)Mj[b + i];
+        lo16[b + i] = (uint16_t)(c & 0xffffu);
+        const int hi = min((int)(c >> 16), nb1);   // (clamped: a column past M's width writes nothing past the row's starts)
+        const int hp = i ? min((int)((uint32_t)Mj[b + i - 1] >> 16), nb1) : 0;
+        for (int q = hp + 1; q <= hi; ++q) st[q - 1] = i;
+    }
+    const int hl = len ? (int)((uint32_t)Mj[b + len - 1] >> 16) : 0;
+    for (int q = hl + 1 + l; q <= nb1; q += WAVE) st[q - 1] = len;
+}
+
+// Join: column = (block << 16) | low half, the block = the number of interior starts <= the
+// entry's offset in its row (the starts ascend; a binary search over the row's nb1 starts).
+template <typename IP>
+__global__ __launch_bounds__(256) void k_cols16_join(int64_t rows, const IP* __restrict__ Mp, int nb1,
+                                                     const uint32_t* __restrict__ starts,
+                                                     const uint16_t* __restrict__ lo16, int32_t* __restrict__ Mj) {
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const int l = lane_id();
+    const int64_t b = (int64_t)Mp[row];
+    const uint32_t len = (uint32_t)((int64_t)Mp[row + 1] - b);
+    const uint32_t* __restrict__ st = starts + row * nb1;
+    for (uint32_t i = l; i < len; i += WAVE) {
+        int lo = 0, hi = nb1;   // first q with st[q] > i
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (st[mid] <= i) lo = mid + 1; else hi = mid;
+        }
+        Mj[b + i] = (int32_t)(((uint32_t)lo << 16) | (uint32_t)lo16[b + i]);
+    }
+}
+
 extern "C" {
 
 int spg_version(void) { return SPG_VERSION_MAJOR * 10000 + SPG_VERSION_MINOR * 100 + SPG_VERSION_PATCH; }
@@ -1959,6 +2007,57 @@ spg_status_t spg_peak_bytes(spg_plan_t p, size_t* bytes) {
     int64_t nnz = p->nnzC >= 0 ? p->nnzC : std::max<int64_t>(p->P, 0);
     *bytes = p->ws_bytes + ipc * (size_t)(p->A.rows + 1) +
              (size_t)nnz * (sizeof(int32_t) + vbytes(p->A.value_type));
+    return SPG_STATUS_SUCCESS;
+}
+
+static spg_status_t check_cols16(const spg_csr_t* M, const void* starts, const void* lo16) {
+    if (!M || M->rows < 0 || M->cols < 0 || M->nnz < 0) return SPG_STATUS_INVALID_VALUE;
+    if (M->cols > 2147483647LL) return SPG_STATUS_NOT_SUPPORTED;
+    if (M->indptr_type != SPG_INDEX_32I && M->indptr_type != SPG_INDEX_64I) return SPG_STATUS_INVALID_VALUE;
+    if (!M->indptr) return SPG_STATUS_INVALID_VALUE;
+    if (M->nnz > 0 && (!M->indices || !lo16)) return SPG_STATUS_INVALID_VALUE;
+    if (M->cols > 65536 && M->rows > 0 && !starts) return SPG_STATUS_INVALID_VALUE;
+    return SPG_STATUS_SUCCESS;
+}
+
+// interior block starts per row: ceil(cols / 65536) - 1 (none for a matrix <= 65536 wide)
+static int cols16_nb1(const spg_csr_t* M) { return (int)std::max<int64_t>(0, (M->cols + 65535) / 65536 - 1); }
+
+spg_status_t spg_cols16_split(spg_handle_t h, const spg_csr_t* M, uint32_t* block_starts, uint16_t* lo16) {
+    if (!h) return SPG_STATUS_NOT_INITIALIZED;
+    spg_status_t st = check_cols16(M, block_starts, lo16);
+    if (st) return st;
+    if (M->rows == 0) return SPG_STATUS_SUCCESS;
+    DeviceGuard dg_(h->device);
+    SPG_HIP(h, dg_.err);
+    const int nb1 = cols16_nb1(M);
+    const dim3 g((unsigned)grid_for(M->rows, 4)), b(256);
+    if (M->indptr_type == SPG_INDEX_64I)
+        timed_launch(h, SPG_PHASE_LAYOUT, k_cols16_split<int64_t>, g, b, M->rows, (const int64_t*)M->indptr,
+                     (const int32_t*)M->indices, nb1, block_starts, lo16);
+    else
+        timed_launch(h, SPG_PHASE_LAYOUT, k_cols16_split<int32_t>, g, b, M->rows, (const int32_t*)M->indptr,
+                     (const int32_t*)M->indices, nb1, block_starts, lo16);
+    SPG_LAUNCHED(h);
+    return SPG_STATUS_SUCCESS;
+}
+
+spg_status_t spg_cols16_join(spg_handle_t h, spg_csr_t* M, const uint32_t* block_starts, const uint16_t* lo16) {
+    if (!h) return SPG_STATUS_NOT_INITIALIZED;
+    spg_status_t st = check_cols16(M, block_starts, lo16);
+    if (st) return st;
+    if (M->rows == 0) return SPG_STATUS_SUCCESS;
+    DeviceGuard dg_(h->device);
+    SPG_HIP(h, dg_.err);
+    const int nb1 = cols16_nb1(M);
+    const dim3 g((unsigned)grid_for(M->rows, 4)), b(256);
+    if (M->indptr_type == SPG_INDEX_64I)
+        timed_launch(h, SPG_PHASE_LAYOUT, k_cols16_join<int64_t>, g, b, M->rows, (const int64_t*)M->indptr, nb1,
+                     block_starts, lo16, (int32_t*)M->indices);
+    else
+        timed_launch(h, SPG_PHASE_LAYOUT, k_cols16_join<int32_t>, g, b, M->rows, (const int32_t*)M->indptr, nb1,
+                     block_starts, lo16, (int32_t*)M->indices);
+    SPG_LAUNCHED(h);
     return SPG_STATUS_SUCCESS;
 }
 

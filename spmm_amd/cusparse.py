@@ -100,6 +100,39 @@ def validate_csr(m: csr_matrix) -> int:
     return res.value
 
 
+def _cols16_nb1(cols: int) -> int:
+    """Interior 65536-column block starts per row (include/spgemm.h, spg_cols16_*)."""
+    return max(0, -(-int(cols) // 65536) - 1)
+
+
+def _cols16_split(m: csr_matrix):
+    """(block_starts int32 [rows, nb1], lo16 int16 [nnz]) of a device CSR (spg_cols16_split)."""
+    rows, nb1 = m.shape[0], _cols16_nb1(m.shape[1])
+    starts = torch.empty((rows, nb1), dtype=torch.int32, device=m.device)
+    lo16 = torch.empty(m.nnz, dtype=torch.int16, device=m.device)
+    h = _handle_for(m)
+    v = SpgCsr(rows, m.shape[1], m.nnz, m.indptr.data_ptr(), m.indices.data_ptr() if m.nnz else 0, 0,
+               _IT[m.indptr.dtype], _VT[torch.float64])
+    check(h.lib.spg_cols16_split(h.ptr, ctypes.byref(v), ctypes.c_void_p(starts.data_ptr() if starts.numel() else 0),
+                                 ctypes.c_void_p(lo16.data_ptr() if m.nnz else 0)), "spg_cols16_split")
+    return starts, lo16
+
+
+def _cols16_join(indptr: torch.Tensor, starts: torch.Tensor, lo16: torch.Tensor, shape) -> torch.Tensor:
+    """int32 column indices from a device (indptr, block starts, low halves) (spg_cols16_join)."""
+    rows, cols = shape
+    nnz = lo16.numel()
+    out = torch.empty(nnz, dtype=torch.int32, device=indptr.device)
+    dev = indptr.device.index if indptr.device.index is not None else torch.cuda.current_device()
+    h = _lib.get_handle(dev)
+    h.set_stream(_current_stream_ptr(dev))
+    v = SpgCsr(rows, cols, nnz, indptr.data_ptr(), out.data_ptr() if nnz else 0, 0, _IT[indptr.dtype],
+               _VT[torch.float64])
+    check(h.lib.spg_cols16_join(h.ptr, ctypes.byref(v), ctypes.c_void_p(starts.data_ptr() if starts.numel() else 0),
+                                ctypes.c_void_p(lo16.data_ptr() if nnz else 0)), "spg_cols16_join")
+    return out
+
+
 _VALUE_DTYPES = (torch.float32, torch.float64, torch.complex64, torch.complex128)
 
 

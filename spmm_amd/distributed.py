@@ -7,7 +7,9 @@ cross-GPU reduction.  The collectives are
 * ``broadcast_csr``: B from ``src`` to every rank: one 6-int64 metadata broadcast (the
   reference's sparse broadcast protocol, modify_src/cupy-src/cupyx/distributed/
   _nccl_comm.py:651-674, metadata exchange :506-530), then the structure (row pointer and
-  column indices packed into ONE buffer; 16-bit columns when B is at most 65536 wide) and the values (a second buffer), each a single
+  column indices packed into ONE buffer; the columns as 16-bit low halves, plus each row's
+  65536-column block starts when B is wider -- spg_cols16_split / spg_cols16_join) and the
+  values (a second buffer), each a single
   RCCL broadcast -- the reference groups its three payload broadcasts between
   groupStart/groupEnd (:669); two packed buffers are the same "few large collectives" on
   torch.distributed.  With ``async_values=True`` the values broadcast is left in flight and
@@ -47,6 +49,37 @@ def _bytes_of(t: torch.Tensor) -> torch.Tensor:
     return t.contiguous().view(-1).view(torch.uint8)
 
 
+def cols16_layout(rows: int, cols: int, nnz: int) -> int:
+    """Interior block starts per row when B's columns travel as 16-bit low halves, or -1
+    when they travel as int32: a matrix at most 65536 wide needs no starts (nb1 = 0); a
+    wider one uses them while 4 bytes per row and block + 2 per entry beat 4 per entry
+    (config 5's B: 141 MB of structure instead of 276 MB)."""
+    from .cusparse import _cols16_nb1
+    nb1 = _cols16_nb1(cols)
+    return nb1 if 4 * rows * nb1 + 2 * nnz < 4 * nnz or nb1 == 0 else -1
+
+
+def _cols16_split_host(M: csr_matrix, nb1: int):
+    """spg_cols16_split's result for a host CSR (the gloo tests' CPU tensors)."""
+    rows = M.shape[0]
+    ip = M.indptr.to(torch.int64)
+    row = torch.repeat_interleave(torch.arange(rows), ip[1:] - ip[:-1])
+    hi = (M.indices.to(torch.int64) >> 16).clamp(max=nb1)
+    cnt = torch.bincount(row * (nb1 + 1) + hi, minlength=rows * (nb1 + 1)).view(rows, nb1 + 1)
+    starts = cnt.cumsum(1)[:, :nb1].to(torch.int32).contiguous()
+    return starts, M.indices.contiguous().view(torch.int16)[0::2].contiguous()
+
+
+def _cols16_join_host(indptr: torch.Tensor, starts: torch.Tensor, lo16: torch.Tensor) -> torch.Tensor:
+    """spg_cols16_join's result on host tensors."""
+    ip = indptr.to(torch.int64)
+    rows = ip.numel() - 1
+    row = torch.repeat_interleave(torch.arange(rows), ip[1:] - ip[:-1])
+    pos = torch.arange(lo16.numel()) - ip[:-1][row]
+    blk = (pos[:, None] >= starts.to(torch.int64)[row]).sum(1) if starts.shape[1] else torch.zeros_like(pos)
+    return ((blk << 16) | (lo16.to(torch.int64) & 0xffff)).to(torch.int32)
+
+
 def broadcast_csr(M: csr_matrix | None, src: int, device, group=None, async_values: bool = False,
                   values: bool = True):
     """Broadcast a CSR matrix held by rank `src` to every rank of `group`.
@@ -66,15 +99,27 @@ def broadcast_csr(M: csr_matrix | None, src: int, device, group=None, async_valu
     rows, cols, nnz, dtc, ipc, _ = (int(x) for x in meta.tolist())
     ipt = _CODE_IP[ipc]
     ib = torch.empty(0, dtype=ipt).element_size()
-    # column indices of a matrix at most 65536 wide travel as their low 16 bits (exact), half
-    # the structure bytes -- the part of the step's broadcast the symbolic pass waits for
-    cb = 2 if cols <= 65536 else 4
-    sbytes = ib * (rows + 1) + cb * nnz          # structure: indptr | indices
+    # column indices travel as their low 16 bits (exact) plus, for a matrix wider than 65536,
+    # each row's 65536-column block starts (cols16_layout): about half the structure bytes --
+    # the part of the step's broadcast every rank waits for before its plan
+    nb1 = cols16_layout(rows, cols, nnz)
+    pbytes = ib * (rows + 1)
+    sbytes = pbytes + (4 * nnz if nb1 < 0 else 4 * rows * nb1 + 2 * nnz)   # indptr | [starts |] indices
+    dev_t = torch.device(device).type
     if rank == src:
-        idx = M.indices.to(device).contiguous()
-        if cb == 2:
-            idx = idx.view(torch.int16)[0::2].contiguous()   # (little-endian: the low halves)
-        struct = torch.cat([_bytes_of(M.indptr.to(device)), _bytes_of(idx)])
+        parts = [_bytes_of(M.indptr.to(device))]
+        if nb1 < 0:
+            parts.append(_bytes_of(M.indices.to(device)))
+        else:
+            Mi = csr_matrix._from_parts(M.data.to(device), M.indices.to(device), M.indptr.to(device), M.shape,
+                                        canonical=True)
+            if dev_t == "cuda":
+                from .cusparse import _cols16_split
+                starts, lo16 = _cols16_split(Mi)
+            else:
+                starts, lo16 = _cols16_split_host(Mi, nb1)
+            parts += [_bytes_of(starts), _bytes_of(lo16)] if nb1 else [_bytes_of(lo16)]
+        struct = torch.cat(parts)
         data = M.data.to(device).contiguous()
     else:
         struct = torch.empty(sbytes, dtype=torch.uint8, device=device)
@@ -86,13 +131,19 @@ def broadcast_csr(M: csr_matrix | None, src: int, device, group=None, async_valu
             work = dist.broadcast(_bytes_of(data), src, group=group, async_op=True)
         else:
             dist.broadcast(_bytes_of(data), src, group=group)
-    indptr = struct[:ib * (rows + 1)].view(ipt)
+    indptr = struct[:pbytes].view(ipt)
     if rank == src:
         indices = M.indices.to(device)
-    elif cb == 2:
-        indices = struct[ib * (rows + 1):].view(torch.int16).to(torch.int32) & 0xffff
+    elif nb1 < 0:
+        indices = struct[pbytes:].view(torch.int32)
     else:
-        indices = struct[ib * (rows + 1):].view(torch.int32)
+        starts = struct[pbytes:pbytes + 4 * rows * nb1].view(torch.int32).view(rows, nb1)
+        lo16 = struct[pbytes + 4 * rows * nb1:].view(torch.int16)
+        if dev_t == "cuda":
+            from .cusparse import _cols16_join
+            indices = _cols16_join(indptr, starts, lo16, (rows, cols))
+        else:
+            indices = _cols16_join_host(indptr, starts, lo16)
     out = csr_matrix._from_parts(data, indices, indptr, (rows, cols), canonical=True)
     return (out, work) if async_values else out
 

@@ -16,7 +16,7 @@ LIB = os.path.join(ROOT, "spmm_amd", "lib", "libmi355_spgemm.so")
 def declared_functions():
     src = open(HEADER).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(spg_[a-z_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(spg_[a-z0-9_]+)\s*\(", src)))
 
 
 def test_header_declares_the_boundary():
@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
     assert os.path.exists(LIB), "run __graft_entry__.build() first"
     out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True,
                          check=True).stdout
-    exported = set(re.findall(r"\bT (spg_[a-z_]+)", out))
+    exported = set(re.findall(r"\bT (spg_[a-z0-9_]+)", out))
     missing = [f for f in declared_functions() if f not in exported]
     assert not missing, missing
 

@@ -197,8 +197,9 @@ def test_tile_groups_cover_and_balance():
 
 
 def _wide_worker(rank, world, port, out):
-    """broadcast_csr on both structure encodings: 16-bit columns (B at most 65536 wide) and
-    32-bit ones (wider), each received exactly."""
+    """broadcast_csr on both structure encodings: 16-bit columns (with each row's 65536-column
+    block starts when B is wider) and 32-bit ones (a B so wide and sparse that the starts
+    would cost more: 10**7 columns, 2 entries per row), each received exactly."""
     import scipy.sparse as sp
     import torch.distributed as dist
     from spmm_amd import distributed
@@ -208,9 +209,10 @@ def _wide_worker(rank, world, port, out):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     cpu = torch.device("cpu")
     ok = []
-    for cols in (65536, 65537, 200000):
+    for cols in (65536, 65537, 200000, 10 ** 7):
         rng = np.random.default_rng(cols)
-        Bh = sp.random(40, cols, density=40.0 / cols, format="csr", random_state=rng)
+        per_row = 2.0 if cols == 10 ** 7 else 40.0
+        Bh = sp.random(40, cols, density=per_row / cols, format="csr", random_state=rng)
         Bh.indices[-1] = cols - 1 if Bh.nnz else 0   # the widest column travels too
         Bh.sort_indices()
         B = distributed.broadcast_csr(csr_matrix(Bh, device=cpu) if rank == 0 else None, 0, cpu)
@@ -225,4 +227,42 @@ def test_broadcast_csr_column_encodings_gloo():
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_wide_worker, args=(2, _free_port(), out), nprocs=2, join=True)
-    assert out[0] == [True] * 3 and out[1] == [True] * 3, dict(out)
+    assert out[0] == [True] * 4 and out[1] == [True] * 4, dict(out)
+    from spmm_amd import distributed
+    assert distributed.cols16_layout(40, 65536, 1600) == 0
+    assert distributed.cols16_layout(40, 200000, 1600) == 3
+    assert distributed.cols16_layout(40, 10 ** 7, 80) == -1
+
+
+def _edge_csr(cols):
+    """Rows that exercise the block starts: empty rows, a row only in the last block, a row
+    on the block edges (c * 65536 - 1, c * 65536), a row in the first block only."""
+    import scipy.sparse as sp
+    nb = -(-cols // 65536)
+    edges = sorted({min(cols - 1, max(0, c * 65536 + d)) for c in range(nb) for d in (-1, 0)})
+    rows = [[], [cols - 1], edges, [0, 5, 65535 if cols > 65535 else cols - 1], [],
+            sorted(set(np.random.default_rng(cols).integers(0, cols, 300).tolist()))]
+    ip = np.cumsum([0] + [len(r) for r in rows])
+    return sp.csr_matrix((np.arange(ip[-1], dtype=np.float64) + 1.0, np.concatenate([np.array(r, dtype=np.int32) for r in rows]),
+                          ip), shape=(len(rows), cols))
+
+
+@pytest.mark.parametrize("cols", [7, 65536, 65537, 131072, 131073, 300000])
+def test_cols16_host_roundtrip(cols):
+    """The host split/join (the CPU tensors of the gloo tests; spg_cols16_split/join on the
+    GPU): starts[r, c-1] = the first entry of row r with column >= c * 65536, and the join
+    gives the columns back exactly."""
+    from spmm_amd import distributed
+    from spmm_amd.sparse import csr_matrix
+    Bh = _edge_csr(cols)
+    M = csr_matrix(Bh, device="cpu")
+    nb1 = max(0, -(-cols // 65536) - 1)
+    starts, lo16 = distributed._cols16_split_host(M, nb1)
+    assert starts.shape == (Bh.shape[0], nb1) and lo16.numel() == Bh.nnz
+    for r in range(Bh.shape[0]):
+        row = Bh.indices[Bh.indptr[r]:Bh.indptr[r + 1]]
+        want = [int(np.searchsorted(row, c * 65536, side="left")) for c in range(1, nb1 + 1)]
+        assert starts[r].tolist() == want, (r, starts[r].tolist(), want)
+    assert np.array_equal(lo16.numpy().view(np.uint16), (Bh.indices & 0xffff).astype(np.uint16))
+    back = distributed._cols16_join_host(M.indptr, starts, lo16)
+    assert back.dtype == torch.int32 and np.array_equal(back.numpy(), Bh.indices)

@@ -164,7 +164,8 @@ dev = torch.device("cuda:0")
 out = {}
 runs = [("sparse8192_f64", 2), ("dense2048_f64", 2), ("c128", 2),
         ("dense2048_f64", 1),      # ALG1: no tile geometry -> the row-major values broadcast
-        ("sparse8192_f64", 3)]     # ALG3 with its chunks forced: several chunks -> the same
+        ("sparse8192_f64", 3),     # ALG3 with its chunks forced: several chunks -> the same
+        ("wide140k_f64", 2)]       # B wider than 65536: 16-bit columns + block starts (spg_cols16_join)
 cases = {c[0]: c for c in _cases()}
 for name, alg in runs:
     _, A, B, alpha = cases[name]
@@ -208,7 +209,7 @@ def test_pipelined_rowblock_two_ranks_one_gpu(tmp_path):
     assert all(p.returncode == 0 for p in procs), "\n".join(l[-3000:] for l in logs)
     cases = {c[0]: c for c in _cases()}
     for name, alg in [("sparse8192_f64", 2), ("dense2048_f64", 2), ("c128", 2), ("dense2048_f64", 1),
-                      ("sparse8192_f64", 3)]:
+                      ("sparse8192_f64", 3), ("wide140k_f64", 2)]:
         _, A, B, alpha = cases[name]
         parts = [np.load(tmp_path / f"{name}_alg{alg}_{r}.npz") for r in range(2)]
         if alg == 2:   # pipelined: 3 value-tile groups on both ranks (fewer value tiles: one each)
@@ -252,3 +253,28 @@ def test_numeric_tiles_argument_errors():
     with pytest.raises(RuntimeError, match="covered"):
         cusparse._spgemm(dA, dB, alg=2, by_tiles=short)
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("ip", [torch.int32, torch.int64])
+def test_cols16_kernels(ip):
+    """spg_cols16_split / spg_cols16_join (the structure broadcast's 16-bit columns) against
+    the host split and the original columns: the block-edge rows of _edge_csr at several
+    widths, and a 20000 x 300000 random B (nnz ~ 2.4M)."""
+    import scipy.sparse as sp
+    from spmm_amd import cusparse, distributed
+    from spmm_amd.sparse import csr_matrix
+    from tests.test_distributed_gloo import _edge_csr
+    mats = [_edge_csr(c) for c in (7, 65536, 65537, 131073, 300000)]
+    mats.append(sp.random(20000, 300000, density=4e-4, format="csr", random_state=np.random.default_rng(3)))
+    for Bh in mats:
+        Bh.sort_indices()
+        M = csr_matrix(Bh, device="cuda:0")
+        M = csr_matrix._from_parts(M.data, M.indices, M.indptr.to(ip), M.shape, canonical=True)
+        nb1 = cusparse._cols16_nb1(Bh.shape[1])
+        starts, lo16 = cusparse._cols16_split(M)
+        hs, hl = distributed._cols16_split_host(csr_matrix(Bh, device="cpu"), nb1)
+        assert torch.equal(starts.cpu(), hs), Bh.shape
+        assert torch.equal(lo16.cpu(), hl), Bh.shape
+        back = cusparse._cols16_join(M.indptr, starts, lo16, Bh.shape)
+        torch.cuda.synchronize()
+        assert back.dtype == torch.int32 and np.array_equal(back.cpu().numpy(), Bh.indices), Bh.shape
