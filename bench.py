@@ -485,8 +485,10 @@ def pipeline_report(ctx, args, A, B, alg, cf, hook, ms):
     rank waits for before its layout and symbolic pass), the step with the values in one
     broadcast that overlaps only the symbolic pass (2 steps), and the step as measured
     (tile-major value groups in flight from before the symbolic pass through the numeric
-    tiles).  hidden_ms = unpipelined - measured; overlap_frac = hidden_ms /
-    values_broadcast_ms.  None on the CPU test path."""
+    tiles), and the pipelined step with the values sent after the symbolic pass (round 4's
+    order).  hidden_ms = unpipelined - measured; overlap_frac = hidden_ms /
+    values_broadcast_ms; symbolic_hidden_ms = values-after-symbolic - measured.  None on the
+    CPU test path."""
     if not ctx.gpu or hook is not None:
         return None
     from spmm_amd import distributed
@@ -533,12 +535,24 @@ def pipeline_report(ctx, args, A, B, alg, cf, hook, ms):
     (el,) = ctx.reduce([el], "max")
     oms = el / 2 * 1e3
     ums, pms = (oms, ms) if pipelined else (ms, oms)
+    lms = None
+    if pipelined:   # the values after the symbolic pass (round 4's order): what sending them first hides
+        def late():
+            C, _ = distributed.rowblock_step(A, B, 0, ctx.dev, alg=alg, chunk_fraction=cf, pipeline=True,
+                                             n_groups=args.value_groups, values_first=False)
+            return C
+        el, C = timed(ctx, late, 2, 1)
+        del C
+        (el,) = ctx.reduce([el], "max")
+        lms = el / 2 * 1e3
     groups = len(last.groups) if (pipelined and last is not None and last.pipelined) else None
     return {"pipelined": pipelined and groups is not None, "groups": groups,
             "values_broadcast_ms": round(vms, 3), "structure_broadcast_ms": round(sms, 3),
             "structure_bytes": sbytes, "values_bytes": nnzB * esz,
             "step_ms_unpipelined": round(ums, 4),
             "step_ms_pipelined": round(pms, 4), "hidden_ms": round(ums - pms, 4),
+            "step_ms_values_after_symbolic": None if lms is None else round(lms, 4),
+            "symbolic_hidden_ms": None if lms is None else round(lms - pms, 4),
             "overlap_frac": round((ums - pms) / vms, 4) if vms > 0 else None}
 
 

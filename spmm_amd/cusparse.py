@@ -162,7 +162,8 @@ def spgemm(a, b, alpha=1, alg=0, chunk_fraction=0.2, verbose=False):
     return _spgemm(a, b, alpha, alg, chunk_fraction, verbose)
 
 
-def _spgemm(a, b, alpha=1, alg=0, chunk_fraction=0.2, verbose=False, before_numeric=None, by_tiles=None):
+def _spgemm(a, b, alpha=1, alg=0, chunk_fraction=0.2, verbose=False, before_numeric=None, by_tiles=None,
+            values_first=True):
     """spgemm, plus `before_numeric`: a callable run after the symbolic pass and before the
     numeric pass reads the values (the multi-GPU path waits there for B's values to arrive
     over RCCL; spmm_amd.distributed).  With it the call takes the ctypes path (the native
@@ -171,7 +172,8 @@ def _spgemm(a, b, alpha=1, alg=0, chunk_fraction=0.2, verbose=False, before_nume
 
     `by_tiles(geom)`: the numeric pass by column-tile groups (spg_numeric_tiles), called
     exactly once per product, BEFORE the symbolic pass (the plan's tile layout needs only
-    B's structure, so B's values can travel while the symbolic pass runs; _spgemm_by_tiles).
+    B's structure, so B's values can travel while the symbolic pass runs; _spgemm_by_tiles;
+    ``values_first=False``: after it, round 4's order, for the bench's comparison).
     `geom` is None when the plan cannot
     run by tiles (not the tile path, several row chunks, ALG1); then `by_tiles` makes
     b.data complete and returns None, and spg_numeric runs.  Otherwise geom is a dict
@@ -216,7 +218,7 @@ def _spgemm(a, b, alpha=1, alg=0, chunk_fraction=0.2, verbose=False, before_nume
             raise RuntimeError("by_tiles must complete B's values when geom is None")
         by_tiles = None
     if by_tiles is not None:
-        return _spgemm_by_tiles(h, a, b, alpha, algo, cf, by_tiles, verbose)
+        return _spgemm_by_tiles(h, a, b, alpha, algo, cf, by_tiles, verbose, values_first)
     if fp is not None:   # the same sequence in one native call (csrc/fastpath.cpp)
         al = complex(alpha)
         st, data, indices, indptr, wsb, peak = fp.spgemm(
@@ -285,7 +287,7 @@ def _alpha_of(dtype, alpha):
     return (ct * 2)(complex(alpha).real, complex(alpha).imag) if nparts == 2 else ct(float(alpha))
 
 
-def _spgemm_by_tiles(h, a, b, alpha, algo, cf, by_tiles, verbose):
+def _spgemm_by_tiles(h, a, b, alpha, algo, cf, by_tiles, verbose, values_first=True):
     """_spgemm with `by_tiles` (the row-block step of spmm_amd.distributed): spg_plan, then
     the tile geometry -- spg_tile_value_offsets builds the plan's tile layout from B's
     structure alone -- and ``by_tiles(geom)``, which starts B's values travelling group by
@@ -306,10 +308,9 @@ def _spgemm_by_tiles(h, a, b, alpha, algo, cf, by_tiles, verbose):
                        ctypes.c_void_p(ws.data_ptr()), ctypes.byref(plan)), "spg_plan")
     al = _alpha_of(a.data.dtype, alpha)
     try:
-        geom = _tile_geometry(h, plan, b)
-        got = by_tiles(geom)
-        if got is not None and geom is None:
-            raise RuntimeError("by_tiles returned tile groups for a plan that cannot run by tiles")
+        if values_first:
+            geom = _tile_geometry(h, plan, b)
+            got = by_tiles(geom)
         nnz = ctypes.c_int64(0)
         wide = a.nnz * (b.nnz / max(b.shape[0], 1)) >= 2 ** 31
         for it in ((torch.int64,) if wide else (torch.int32, torch.int64)):
@@ -318,6 +319,11 @@ def _spgemm_by_tiles(h, a, b, alpha, algo, cf, by_tiles, verbose):
             if st != _lib.STATUS_OVERFLOW:
                 break
         check(st, "spg_symbolic")
+        if not values_first:
+            geom = _tile_geometry(h, plan, b)
+            got = by_tiles(geom)
+        if got is not None and geom is None:
+            raise RuntimeError("by_tiles returned tile groups for a plan that cannot run by tiles")
         nnzc = int(nnz.value)
         indices = torch.empty(nnzc, dtype=torch.int32, device=dev)
         data = torch.empty(nnzc, dtype=a.data.dtype, device=dev)

@@ -332,14 +332,15 @@ class StepReport:
 
 def rowblock_step(A_block: csr_matrix, B_src: csr_matrix | None, src: int, device, alg: int = 2,
                   chunk_fraction: float = 0.2, multiply=None, group=None, pipeline: bool | None = None,
-                  n_groups: int = 8):
+                  n_groups: int = 8, values_first: bool = True):
     """One C = A.B step of the row-block scheme on this rank: B arrives from `src` (its
     structure first; the values stay in flight through the symbolic pass and, pipelined,
     the numeric tiles), then this
     rank's slab A_block . B.  `multiply(A_block, B, wait_values)` replaces the device
     multiply (the gloo tests run the CPU oracle there).  `pipeline` (default: on a GPU
     device): the values travel tile-major in `n_groups` async broadcasts, each group's
-    numeric tiles starting as its slice lands (TileValueBroadcast).
+    numeric tiles starting as its slice lands (TileValueBroadcast); `values_first` (default)
+    sends them before the symbolic pass, False after it (round 4's order, for comparison).
 
     Returns (C slab, B).  After a pipelined step B's values exist row-major on `src` only,
     so the other ranks get None for B (their B never held row-major values).  A_block is
@@ -357,7 +358,8 @@ def rowblock_step(A_block: csr_matrix, B_src: csr_matrix | None, src: int, devic
             tv = TileValueBroadcast(B, src, device, group, n_groups)
             from . import cusparse
             try:
-                C = cusparse._spgemm(A_block, B, alg=alg, chunk_fraction=chunk_fraction, by_tiles=tv)
+                C = cusparse._spgemm(A_block, B, alg=alg, chunk_fraction=chunk_fraction, by_tiles=tv,
+                                     values_first=values_first)
             finally:
                 tv.finish()
             rowblock_step.last = tv.report()

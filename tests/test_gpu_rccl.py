@@ -8,7 +8,8 @@ on RCCL's own stream and the ``work.wait()`` ordering of the numeric tiles after
 RCCL takes one rank per GPU, so on a one-GPU box this is a world of size 1: every
 collective runs through RCCL's kernels and streams, with rank 0 as the broadcast source.
 Run in a child process (a fresh process group, bounded by a timeout); the C slabs of
-``pipeline=True`` and ``pipeline=False`` are checked bit for bit against the oracle.
+``pipeline=True`` (values before the symbolic pass, and after it: ``values_first=False``) and
+``pipeline=False`` are checked bit for bit against the oracle.
 """
 import os
 import socket
@@ -41,19 +42,21 @@ report = {}
 for name in ("dense2048_f64", "sparse8192_f64"):
     _, A, B, alpha = cases[name]
     dA = csr_matrix(A, device=dev)
-    for pipe in (True, False):
+    for pipe in (True, False, "late"):   # late: the values after the symbolic pass
         B_src = csr_matrix(B, device=dev)
         (r0, r1), A_blk, _ = distributed.rowblock_setup(dA, B_src.indptr, 1, 0)
         for rep in range(2):   # a second step reuses RCCL's communicator and buffers
-            C, Bo = distributed.rowblock_step(A_blk, B_src, 0, dev, alg=2, pipeline=pipe, n_groups=3)
+            C, Bo = distributed.rowblock_step(A_blk, B_src, 0, dev, alg=2, pipeline=bool(pipe), n_groups=3,
+                                              values_first=pipe != "late")
         torch.cuda.synchronize()
         last = distributed.rowblock_step.last
         from spmm_amd import cusparse
         info = cusparse.plan_info(A_blk, B_src, alg=2)
         vt = -(-info["tiles_per_row"] // info["record_group"])   # value tiles (record groups)
-        report[f"{name}_{int(pipe)}"] = {"pipelined": bool(last.pipelined), "groups": len(last.groups),
+        key = pipe if pipe == "late" else int(pipe)
+        report[f"{name}_{key}"] = {"pipelined": bool(last.pipelined), "groups": len(last.groups),
                                          "b_returned": Bo is not None, "value_tiles": vt}
-        np.savez(os.path.join(OUT, f"{name}_{int(pipe)}.npz"), p=C.indptr.cpu().numpy().astype(np.int64),
+        np.savez(os.path.join(OUT, f"{name}_{key}.npz"), p=C.indptr.cpu().numpy().astype(np.int64),
                  j=C.indices.cpu().numpy(), x=C.data.cpu().numpy())
     # agree_tiles on device tensors: a plan off the tile path disagrees, a tile plan agrees
     assert distributed.agree_tiles(None, dev) is False
@@ -90,7 +93,7 @@ def test_rowblock_step_over_rccl_world1(tmp_path):
     for name in ("dense2048_f64", "sparse8192_f64"):
         _, A, B, _ = cases[name]
         rp, rj, rx = oracle.spgemm(A, B, keep_zeros=True, sort=True, threads=16)
-        for pipe in (1, 0):
+        for pipe in (1, 0, "late"):
             r = report[f"{name}_{pipe}"]
             assert r["pipelined"] == bool(pipe), (name, r)
             assert r["groups"] == (min(3, r["value_tiles"]) if pipe else 0), (name, r)
