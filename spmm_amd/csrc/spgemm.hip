@@ -1558,9 +1558,13 @@ spg_status_t spg_plan(spg_handle_t h, const spg_csr_t* A, const spg_csr_t* B, sp
         tmp.twss = sym_tile_log2(*B, tmp.tws, &tmp.sym_seg);
         tmp.rgs = record_group_log2(tmp);
     }
-    // spills are rare for the shapes the short kernel is chosen for (A rows > 64 entries or
-    // C wider than 16384 columns): a small grid keeps the usually-empty launch cheap
-    tmp.list_grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(64, grid_for(A->rows, 1024)));
+    // the general kernel's launch over the spill list (rows the short kernels hand over: A
+    // rows > 64 entries, C wider than 16384 columns, or a row whose repeated columns overflow
+    // the register path's list -- narrow C rows, e.g. N = 1024 at density 0.01, where dozens of
+    // rows spill).  It runs only when the list is non-empty; one wave per 16 rows of A up to
+    // 1024 waves, so the listed rows run side by side (one 4-wave block per 1024 rows put
+    // them in series: 96 us for the N = 1024 fp32 product above, against 37 us without spills)
+    tmp.list_grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(256, grid_for(A->rows, 64)));
     // ALG1 and ALG3 size their buffers / chunks from the product counts, which needs the
     // device once.  The size query and the building call of one plan see the same
     // operands, so the building call reuses what the query measured.
