@@ -643,10 +643,12 @@ inline bool fp32_runs(const spg_plan_s& p) {
 // Measured on config 5 (round 5, numeric ms per product): RG 1 97.6 (511 GB of fabric reads per
 // launch); RG 4 with one block per item 103 (361 GB: the block's waves idle until its slowest
 // item ends, and a new block needs a whole block's LDS); RG 4 persistent 92.7 (367 GB), RG 8
-// persistent 91.8, RG 2 persistent 101.3; RG 1 persistent 118.5 (one-wave blocks balance best
-// dispatched one item each).  SPG_SP_RGS=0 builds keep RG = 1.
+// persistent 91.8 (301 GB), RG 2 persistent 101.3; RG 1 persistent 118.5 (one-wave blocks
+// balance best dispatched one item each).  On the final kernels (saddr record loads), alternated
+// on one box: RG 8 89.7-89.8 against RG 4 91.0-91.3 (abtest/r05_call24.sh) -- RG 8, one 8-wave
+// block per CU (159.6 KiB of LDS).  SPG_SP_RGS=0 builds keep RG = 1.
 #ifndef SPG_SP_RGS
-#define SPG_SP_RGS 2
+#define SPG_SP_RGS 3
 #endif
 // (SPG_SP_RECORD_GROUP=1, read per plan: a schedule-only switch to the one-wave kernel over
 // plain tile-major records, for A/B timing and for the tests; results are identical)

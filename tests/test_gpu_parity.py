@@ -359,8 +359,8 @@ def _random_rows(rng, rows, cols, per_row):
 
 
 def test_tile_path_cooperative_groups_with_padding():
-    """Config 5's cooperative record groups on a shape whose tile count does not divide by 4:
-    300000 columns -> 37 numeric tiles of 8192 (record groups of 4: the last holds 1 real tile
+    """Config 5's cooperative record groups on a shape whose tile count does not divide by 8:
+    300000 columns -> 37 numeric tiles of 8192 (record groups of 8: the last holds 5 real tiles
     and 3 padding tiles), 5 symbolic tiles of 65536.  Bit-exact for ALG2 and chunked ALG3, and
     the same with the one-wave kernel (SPG_SP_RECORD_GROUP=1)."""
     from spmm_amd import cusparse
@@ -371,7 +371,7 @@ def test_tile_path_cooperative_groups_with_padding():
     B = _random_rows(rng, n, n, 60)
     dA, dB = csr_matrix(A, device=_dev()), csr_matrix(B, device=_dev())
     info = cusparse.plan_info(dA, dB, alg=2)
-    assert info["tile_width"] == 8192 and info["tiles_per_row"] == 37 and info["record_group"] == 4, info
+    assert info["tile_width"] == 8192 and info["tiles_per_row"] == 37 and info["record_group"] == 8, info
     ref = oracle.spgemm(A, B, alpha=1.5, keep_zeros=True, sort=True, threads=16)
     for alg, cf in [(2, 0.2), ("3c", 0.1)]:
         _assert_same(_gpu(A, B, alg=alg, alpha=1.5, cf=cf), ref)
@@ -403,9 +403,9 @@ def test_tile_path_sparse_8192():
     dA, dB = csr_matrix(A, device=_dev()), csr_matrix(B, device=_dev())
     info = cusparse.plan_info(dA, dB, alg=2)
     assert info["tile_width"] == 8192 and not info["dense_tiles"], info
-    # cooperative record groups of 4 tiles (k_tile_sp<.., SpCfgRG, 4>): G = 5 tiles, so the
-    # second group holds one real tile and three padding tiles
-    assert info["record_group"] == 4 and info["tiles_per_row"] == 5, info
+    # cooperative record groups of 8 tiles (k_tile_sp<.., SpCfgRG, 8>): G = 5 tiles, so the
+    # one group holds five real tiles and three padding tiles
+    assert info["record_group"] == 8 and info["tiles_per_row"] == 5, info
     ref = oracle.spgemm(A, B, alpha=0.5, keep_zeros=True, sort=True)
     assert np.diff(ref[0]).max() > 2 * 2048 * 4   # dense rows: several windows per item
     for alg, cf in [(1, 0.2), (2, 0.2), (3, 0.2), ("3c", 0.02)]:
