@@ -375,7 +375,8 @@ __device__ __forceinline__ void dn_emit(DnLds<T, TWD>& S, int l, int TW, int lo,
             for (int e = 0; e < 4; ++e) {
                 const unsigned long long m = __ballot(h[e]);
                 if (h[e] && (SPG_TILE_DIAG & 8) == 0) {   // (diag 8, timing only: no output)
-                    const uint32_t p = (uint32_t)(run + lane_rank(m));
+                    uint32_t p = (uint32_t)(run + lane_rank(m));
+                    if constexpr ((SPG_TILE_DIAG & 128) != 0) p &= 63u;   // (diag 128: the same stores, L2-resident)
                     st_c(crow + p, (int32_t)(lo + (k0 + e) * WAVE + l));
                     st_c(xrow + p, decltype(one)::value ? v[e] : mul_rn(alpha, v[e]));
                 }

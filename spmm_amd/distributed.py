@@ -4,7 +4,7 @@ Rows of C depend only on the same rows of A and on all of B, so each
 owns a contiguous row block of A, receives B, and writes its own C slab -- there is no
 cross-GPU reduction.  The collectives are
 
-* ``broadcast_csr``: B from ``src`` to every rank: one 6-int64 metadata broadcast (the
+* ``broadcast_csr``: B from ``src`` to every rank: one 7-int64 metadata broadcast (the
   reference's sparse broadcast protocol, modify_src/cupy-src/cupyx/distributed/
   _nccl_comm.py:651-674, metadata exchange :506-530), then the structure (row pointer and
   column indices packed into ONE buffer; the columns as 16-bit low halves, plus each row's
@@ -22,8 +22,10 @@ cross-GPU reduction.  The collectives are
   broadcast per group of column tiles, BEFORE the symbolic pass, which runs while they
   travel; each group's numeric tiles (spg_numeric_tiles) start when its slice lands, so
   the values broadcast overlaps the symbolic pass and the numeric pass.  The ranks first
-  agree (one 4-int64 all_gather) that every plan runs by tiles with the same tile width;
-  otherwise the step falls back to the row-major values broadcast and spg_numeric;
+  agree (one 4-int64 all_gather that every rank reaches exactly once per step, a local
+  failure included) that every plan runs by tiles with the same tile width; otherwise the
+  step falls back to the row-major values broadcast and spg_numeric, and a rank that failed
+  before the agreement makes every rank raise (StepFailed) rather than hang;
 * ``allgather_nnz``: every rank's nnz(C slab) -> global row-pointer offsets, when a
   stitched C is wanted.
 
@@ -80,6 +82,19 @@ def _cols16_join_host(indptr: torch.Tensor, starts: torch.Tensor, lo16: torch.Te
     return ((blk << 16) | (lo16.to(torch.int64) & 0xffff)).to(torch.int32)
 
 
+def _rows_sorted(M: csr_matrix) -> bool:
+    """Column indices non-decreasing inside every row (what the 16-bit column encoding
+    needs; duplicates are fine).  One device reduction and one host read."""
+    if M._canonical is True or M.nnz < 2:
+        return True
+    idx = M.indices.to(torch.int64)
+    ok = idx[1:] >= idx[:-1]
+    starts = M.indptr[1:-1].to(torch.int64)   # first entry of rows 1..m-1
+    starts = starts[(starts > 0) & (starts < M.nnz)]
+    ok[starts - 1] = True                      # a row boundary may step down
+    return bool(ok.all())
+
+
 def broadcast_csr(M: csr_matrix | None, src: int, device, group=None, async_values: bool = False,
                   values: bool = True):
     """Broadcast a CSR matrix held by rank `src` to every rank of `group`.
@@ -88,21 +103,29 @@ def broadcast_csr(M: csr_matrix | None, src: int, device, group=None, async_valu
     broadcast is still in flight and ``work.wait()`` orders the current stream after it
     (``work`` is None when there is nothing to wait for).  ``values=False`` broadcasts the
     structure only: off `src` the matrix's values are an uninitialised buffer (filled later,
-    e.g. by ``send_values``)."""
+    e.g. by ``send_values``).
+
+    The metadata carries the column encoding `src` chose (so every rank decodes what was
+    sent) and `src`'s canonical flag: a B whose rows are not sorted travels with int32
+    columns, exactly in its stored order, and arrives marked as `src` knew it."""
     rank = dist.get_rank(group)
-    meta = torch.zeros(6, dtype=torch.int64, device=device)
+    meta = torch.zeros(7, dtype=torch.int64, device=device)
     if rank == src:
+        # column indices travel as their low 16 bits (exact) plus, for a matrix wider than
+        # 65536, each row's 65536-column block starts (cols16_layout): about half the
+        # structure bytes -- the part of the step's broadcast every rank waits for before its
+        # plan.  The encoding needs rows sorted by column; otherwise int32 (nb1 = -1).
+        nb1 = cols16_layout(M.shape[0], M.shape[1], M.nnz)
+        if nb1 > 0 and not _rows_sorted(M):
+            nb1 = -1
+        canon = {True: 1, False: 0, None: -1}[M._canonical]
         meta = torch.tensor([M.shape[0], M.shape[1], M.nnz, _DT_CODE[M.data.dtype],
-                             _IP_CODE[M.indptr.dtype], M.data.element_size()],
-                            dtype=torch.int64, device=device)
+                             _IP_CODE[M.indptr.dtype], nb1, canon], dtype=torch.int64, device=device)
     dist.broadcast(meta, src, group=group)
-    rows, cols, nnz, dtc, ipc, _ = (int(x) for x in meta.tolist())
+    rows, cols, nnz, dtc, ipc, nb1, canon = (int(x) for x in meta.tolist())
+    canonical = {1: True, 0: False, -1: None}[canon]
     ipt = _CODE_IP[ipc]
     ib = torch.empty(0, dtype=ipt).element_size()
-    # column indices travel as their low 16 bits (exact) plus, for a matrix wider than 65536,
-    # each row's 65536-column block starts (cols16_layout): about half the structure bytes --
-    # the part of the step's broadcast every rank waits for before its plan
-    nb1 = cols16_layout(rows, cols, nnz)
     pbytes = ib * (rows + 1)
     sbytes = pbytes + (4 * nnz if nb1 < 0 else 4 * rows * nb1 + 2 * nnz)   # indptr | [starts |] indices
     dev_t = torch.device(device).type
@@ -112,7 +135,7 @@ def broadcast_csr(M: csr_matrix | None, src: int, device, group=None, async_valu
             parts.append(_bytes_of(M.indices.to(device)))
         else:
             Mi = csr_matrix._from_parts(M.data.to(device), M.indices.to(device), M.indptr.to(device), M.shape,
-                                        canonical=True)
+                                        canonical=M._canonical)
             if dev_t == "cuda":
                 from .cusparse import _cols16_split
                 starts, lo16 = _cols16_split(Mi)
@@ -144,7 +167,7 @@ def broadcast_csr(M: csr_matrix | None, src: int, device, group=None, async_valu
             indices = _cols16_join(indptr, starts, lo16, (rows, cols))
         else:
             indices = _cols16_join_host(indptr, starts, lo16)
-    out = csr_matrix._from_parts(data, indices, indptr, (rows, cols), canonical=True)
+    out = csr_matrix._from_parts(data, indices, indptr, (rows, cols), canonical=canonical)
     return (out, work) if async_values else out
 
 
@@ -251,18 +274,40 @@ def tile_groups(offsets, n_groups: int):
     return [(cuts[i], cuts[i + 1]) for i in range(k)]
 
 
-def agree_tiles(geom, device, group=None) -> bool:
-    """Every rank's plan runs by tiles with the same tile width, tile count and value type
-    (one 4-int64 all_gather; a collective every rank calls once per step)."""
+class StepFailed(RuntimeError):
+    """A rank of the step failed before the ranks agreed on how B's values travel; every
+    rank raises this (or the failing rank its own error) instead of blocking in a collective
+    its peers never enter."""
+
+
+# agreement codes (the first word of agree_tiles' all_gather)
+_AGREE_TILES, _AGREE_ROWMAJOR, _AGREE_FAILED = 1, 0, -1
+
+
+def agree_tiles(geom, device, group=None, failed: bool = False) -> bool:
+    """The one agreement of a pipelined step, reached by every rank exactly once (one 4-int64
+    all_gather): True when every rank's plan runs by tiles with the same tile width, tile
+    count and value type; False when some rank cannot (``geom`` None: not the tile path, ALG1,
+    several row chunks, an A block that promotes B) -- the values then go row-major to all.
+    A rank that failed locally before this point reports ``failed=True``; every rank then
+    raises StepFailed, so no rank is left in a collective its peers skip."""
     world = dist.get_world_size(group)
     if dist.get_backend(group) != "nccl":
         device = "cpu"   # gloo (the rehearsal on one GPU) gathers host tensors
-    mine = torch.tensor([1, geom["tile_width"], geom["tiles"], _DT_CODE[geom["dtype"]]] if geom is not None
-                        else [0, 0, 0, -1], dtype=torch.int64, device=device)
+    if failed:
+        words = [_AGREE_FAILED, 0, 0, -1]
+    elif geom is None:
+        words = [_AGREE_ROWMAJOR, 0, 0, -1]
+    else:
+        words = [_AGREE_TILES, geom["tile_width"], geom["tiles"], _DT_CODE[geom["dtype"]]]
+    mine = torch.tensor(words, dtype=torch.int64, device=device)
     out = [torch.zeros(4, dtype=torch.int64, device=device) for _ in range(world)]
     dist.all_gather(out, mine, group=group)
     rows = [tuple(int(v) for v in t.tolist()) for t in out]
-    return rows[0][0] == 1 and all(r == rows[0] for r in rows)
+    bad = [r for r, w in enumerate(rows) if w[0] == _AGREE_FAILED]
+    if bad:
+        raise StepFailed(f"rank(s) {bad} failed before the values broadcast; the step is abandoned on every rank")
+    return rows[0][0] == _AGREE_TILES and all(r == rows[0] for r in rows)
 
 
 class TileValueBroadcast:
@@ -272,16 +317,22 @@ class TileValueBroadcast:
     on (the current stream is ordered after it).  On disagreement the row-major values go
     out in one broadcast and spg_numeric runs.  After the product, `overlap` holds
     (groups, values bytes) for the report; `finish()` orders the current stream after
-    every broadcast (the source's numeric tiles do not wait for its own sends)."""
+    every broadcast (the source's numeric tiles do not wait for its own sends).
+
+    Every rank calls it (or `fail`) exactly once per step: `agreed` records that it did."""
 
     def __init__(self, B: csr_matrix, src: int, device, group=None, n_groups: int = 8):
         self.B, self.src, self.device, self.group, self.n_groups = B, src, device, group, n_groups
         self.works = []
         self.pipelined = False
+        self.agreed = False
         self.groups = []
 
     def __call__(self, geom):
+        if self.agreed:
+            raise RuntimeError("TileValueBroadcast called twice in one step")
         rank = dist.get_rank(self.group)
+        self.agreed = True
         if not agree_tiles(geom, self.device, self.group):
             if self.B.nnz:
                 dist.broadcast(_bytes_of(self.B.data), self.src, group=self.group)
@@ -301,6 +352,16 @@ class TileValueBroadcast:
                          if b > a else None)
         self.works = works
         return tm, self._release(rank)
+
+    def fail(self):
+        """This rank failed before reaching the agreement: tell the others (they raise
+        StepFailed); the caller re-raises its own error.  A no-op once the rank has agreed."""
+        if not self.agreed:
+            self.agreed = True
+            try:
+                agree_tiles(None, self.device, self.group, failed=True)
+            except StepFailed:
+                pass   # (this rank raises its own error)
 
     def _release(self, rank):
         for (g0, g1), w in zip(self.groups, self.works):
@@ -330,9 +391,18 @@ class StepReport:
         self.pipelined, self.groups = pipelined, groups
 
 
+def _device_multiply_tiles(A_block, B, alg, chunk_fraction, by_tiles, values_first):
+    """The pipelined step's device multiply (rowblock_step's `multiply_tiles` default)."""
+    if by_tiles is None:
+        return spgemm_rowblock(A_block, B, alg, chunk_fraction)
+    from . import cusparse
+    return cusparse._spgemm(A_block, B, alg=alg, chunk_fraction=chunk_fraction, by_tiles=by_tiles,
+                            values_first=values_first)
+
+
 def rowblock_step(A_block: csr_matrix, B_src: csr_matrix | None, src: int, device, alg: int = 2,
                   chunk_fraction: float = 0.2, multiply=None, group=None, pipeline: bool | None = None,
-                  n_groups: int = 8, values_first: bool = True):
+                  n_groups: int = 8, values_first: bool = True, multiply_tiles=None):
     """One C = A.B step of the row-block scheme on this rank: B arrives from `src` (its
     structure first; the values stay in flight through the symbolic pass and, pipelined,
     the numeric tiles), then this
@@ -345,31 +415,44 @@ def rowblock_step(A_block: csr_matrix, B_src: csr_matrix | None, src: int, devic
     Returns (C slab, B).  After a pipelined step B's values exist row-major on `src` only,
     so the other ranks get None for B (their B never held row-major values).  A_block is
     cast to B's value type when that type is the common one; otherwise (B would have to be
-    promoted after its values arrive) the step takes the row-major values broadcast."""
+    promoted after its values arrive) this rank votes for the row-major values broadcast in
+    the one agreement every rank reaches (agree_tiles), and every rank takes it.
+
+    Failure before the agreement (planning, the tile layout, the symbolic pass of the
+    values-after order, ...) on any rank makes every rank raise (StepFailed on the others)
+    instead of leaving them in a collective; failure after it leaves the peers' step intact
+    (the failing rank still waits for its outstanding broadcasts).
+
+    `multiply_tiles(A_block, B, alg, chunk_fraction, by_tiles, values_first)` replaces the
+    pipelined device multiply (cusparse._spgemm with `by_tiles`; ``by_tiles=None``: B's
+    values are complete row-major) -- the gloo tests drive the protocol through a CPU one."""
     if pipeline is None:
         pipeline = multiply is None and torch.device(device).type == "cuda"
     if pipeline and multiply is None:
         B, _ = broadcast_csr(B_src, src, device, group, async_values=True, values=False)
-        if A_block.data.dtype != B.data.dtype:
-            common = np.promote_types(A_block.dtype, B.dtype)
-            if common == B.dtype:
-                A_block = A_block.astype(common)
-        if A_block.data.dtype == B.data.dtype:
-            tv = TileValueBroadcast(B, src, device, group, n_groups)
-            from . import cusparse
-            try:
-                C = cusparse._spgemm(A_block, B, alg=alg, chunk_fraction=chunk_fraction, by_tiles=tv,
-                                     values_first=values_first)
-            finally:
-                tv.finish()
-            rowblock_step.last = tv.report()
-            rank = dist.get_rank(group)
-            return C, (B if (rank == src or not tv.pipelined) else None)
-        # mixed value types that promote B: the values row-major, then the shim promotes both
-        if B.nnz:
-            dist.broadcast(_bytes_of(B.data), src, group=group)
-        rowblock_step.last = StepReport(False, [])
-        return spgemm_rowblock(A_block, B, alg, chunk_fraction), B
+        tv = TileValueBroadcast(B, src, device, group, n_groups)
+        mul = multiply_tiles or _device_multiply_tiles
+        try:
+            if A_block.data.dtype != B.data.dtype:
+                common = np.promote_types(A_block.dtype, B.dtype)
+                if common == B.dtype:
+                    A_block = A_block.astype(common)
+            if A_block.data.dtype == B.data.dtype:
+                C = mul(A_block, B, alg, chunk_fraction, tv, values_first)
+            else:
+                # B must be promoted after its values arrive: vote for the row-major values
+                tv(None)
+                C = mul(A_block, B, alg, chunk_fraction, None, values_first)
+        except StepFailed:
+            raise
+        except BaseException:
+            tv.fail()   # (a no-op after the agreement)
+            raise
+        finally:
+            tv.finish()
+        rowblock_step.last = tv.report()
+        rank = dist.get_rank(group)
+        return C, (B if (rank == src or not tv.pipelined) else None)
     B, work = broadcast_csr(B_src, src, device, group, async_values=True)
     wait = work.wait if work is not None else (lambda: None)
     rowblock_step.last = StepReport(False, [])

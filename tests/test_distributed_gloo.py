@@ -266,3 +266,152 @@ def test_cols16_host_roundtrip(cols):
     assert np.array_equal(lo16.numpy().view(np.uint16), (Bh.indices & 0xffff).astype(np.uint16))
     back = distributed._cols16_join_host(M.indptr, starts, lo16)
     assert back.dtype == torch.int32 and np.array_equal(back.numpy(), Bh.indices)
+
+
+def _cpu_tiles_hook(rank, fail_rank=None, tw=64):
+    """rowblock_step's `multiply_tiles` on the CPU: the by_tiles protocol of
+    cusparse._spgemm_by_tiles (geometry from B's structure -> by_tiles(geom) -> groups as
+    they land -> values back to row-major) around the oracle.  `fail_rank` raises where
+    spg_tile_value_offsets would fail, before the agreement."""
+    from oracle import oracle
+
+    def hook(A_b, B, alg, cf, by_tiles, values_first):
+        if by_tiles is None:   # row-major values complete (a rank whose A promotes B)
+            return oracle.spgemm(A_b.get(), B.get(), keep_zeros=True, sort=True)
+        if rank == fail_rank:
+            raise RuntimeError("injected spg_tile_value_offsets failure")
+        Bh = B.get()
+        G = (Bh.shape[1] + tw - 1) // tw
+        rows = np.repeat(np.arange(Bh.shape[0]), np.diff(Bh.indptr))
+        t = Bh.indices // tw
+        order = np.lexsort((np.arange(Bh.nnz), rows, t))
+        offs = np.zeros(G + 1, dtype=np.int64)
+        np.cumsum(np.bincount(t, minlength=G), out=offs[1:])
+        geom = {"tile_width": tw, "tiles": G, "offsets": offs, "dtype": B.data.dtype,
+                "tile_values": lambda: B.data[torch.from_numpy(order)].contiguous()}
+        got = by_tiles(geom)
+        if got is not None:
+            tm, groups = got
+            for _ in groups:
+                pass
+            vals = torch.empty_like(tm)
+            vals[torch.from_numpy(order)] = tm
+            Bh.data = vals.numpy()
+        else:
+            Bh = B.get()
+        return oracle.spgemm(A_b.get(), Bh, keep_zeros=True, sort=True)
+    return hook
+
+
+def _hazard_worker(rank, world, port, mode, out):
+    """Multi-rank hazards of the pipelined step: ranks whose A blocks have
+    different value types, and a rank that fails before the agreement.  Every rank must
+    finish the step (bit-exact) or raise; none may block in a collective its peers skip --
+    the follow-up step proves the group's collectives are still aligned."""
+    import scipy.sparse as sp
+    import torch.distributed as dist
+    from oracle import oracle
+    from spmm_amd import distributed
+    from spmm_amd.sparse import csr_matrix
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cpu = torch.device("cpu")
+    rng = np.random.default_rng(5)
+    Ah = sp.random(120, 700, density=0.03, format="csr", random_state=rng)
+    Bh = sp.random(700, 900, density=0.03, format="csr", random_state=rng)
+    Ah.sort_indices(); Bh.sort_indices()
+    blk = Ah[rank * 60:(rank + 1) * 60]
+    if mode == "dtype" and rank == 1:
+        blk = blk.astype(np.complex128)
+        blk.data = blk.data + 1j * rng.standard_normal(blk.nnz)
+    A_b = csr_matrix(blk, device=cpu)
+    B_src = csr_matrix(Bh, device=cpu) if rank == 0 else None
+    res = {}
+    try:
+        (p, j, x), _ = distributed.rowblock_step(A_b, B_src, 0, cpu, pipeline=True,
+                                                 multiply_tiles=_cpu_tiles_hook(rank, 1 if mode == "fail" else None))
+        rp, rj, rx = oracle.spgemm(blk, Bh, keep_zeros=True, sort=True)
+        res["exact"] = bool(np.array_equal(p, rp) and np.array_equal(j, rj) and x.dtype == rx.dtype
+                            and np.array_equal(x.view(np.uint8), rx.view(np.uint8)))
+        res["pipelined"] = distributed.rowblock_step.last.pipelined
+    except Exception as e:   # noqa: BLE001 -- the test reports which error each rank raised
+        res["raised"] = type(e).__name__
+        res["msg"] = str(e)
+    # a normal pipelined step afterwards: the ranks' collectives are still aligned
+    A_ok = csr_matrix(Ah[rank * 60:(rank + 1) * 60], device=cpu)
+    (p, j, x), _ = distributed.rowblock_step(A_ok, B_src, 0, cpu, pipeline=True, multiply_tiles=_cpu_tiles_hook(rank))
+    rp, rj, rx = oracle.spgemm(Ah[rank * 60:(rank + 1) * 60], Bh, keep_zeros=True, sort=True)
+    res["after"] = bool(np.array_equal(j, rj) and np.array_equal(x.view(np.uint8), rx.view(np.uint8))
+                        and distributed.rowblock_step.last.pipelined)
+    out[rank] = res
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("mode", ["dtype", "fail"])
+def test_rowblock_step_hazards_gloo(mode):
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_hazard_worker, args=(2, _free_port(), mode, out), nprocs=2, join=True)
+    r0, r1 = out[0], out[1]
+    if mode == "dtype":
+        # rank 1's complex A block would promote B: everyone takes the row-major values
+        assert r0.get("exact") and r1.get("exact"), (r0, r1)
+        assert r0["pipelined"] is False and r1["pipelined"] is False
+    else:
+        assert r1.get("raised") == "RuntimeError" and "injected" in r1["msg"], r1
+        assert r0.get("raised") == "StepFailed", r0
+    assert r0["after"] and r1["after"], (r0, r1)
+
+
+def _unsorted_worker(rank, world, port, out):
+    """a B wider than 65536 columns whose rows are NOT sorted must arrive exactly
+    as stored (int32 columns), not through the 16-bit encoding that needs sorted rows."""
+    import scipy.sparse as sp
+    import torch.distributed as dist
+    from spmm_amd import distributed
+    from spmm_amd.sparse import csr_matrix
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cpu = torch.device("cpu")
+    rng = np.random.default_rng(9)
+    Bh = sp.random(50, 200000, density=60 / 200000, format="csr", random_state=rng)
+    Bh.sort_indices()
+    for r in range(0, 50, 3):   # reverse some rows
+        a, b = Bh.indptr[r], Bh.indptr[r + 1]
+        Bh.indices[a:b] = Bh.indices[a:b][::-1].copy()
+        Bh.data[a:b] = Bh.data[a:b][::-1].copy()
+    Bh.has_sorted_indices = False
+    src = csr_matrix((torch.from_numpy(Bh.data), torch.from_numpy(Bh.indices), torch.from_numpy(Bh.indptr)),
+                     shape=Bh.shape, canonical=False) if rank == 0 else None
+    B = distributed.broadcast_csr(src, 0, cpu)
+    out[rank] = (bool(np.array_equal(B.indices.numpy(), Bh.indices) and np.array_equal(B.data.numpy(), Bh.data)),
+                 B._canonical)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_broadcast_csr_unsorted_wide_gloo():
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_unsorted_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    assert out[0] == (True, False) and out[1] == (True, False), dict(out)
+    from spmm_amd import distributed
+    from spmm_amd.sparse import csr_matrix
+    import scipy.sparse as sp
+    S = sp.random(30, 100000, density=1e-3, format="csr", random_state=np.random.default_rng(1))
+    S.sort_indices()
+    assert distributed._rows_sorted(csr_matrix(S, device="cpu"))
+    M = csr_matrix((torch.from_numpy(S.data), torch.from_numpy(S.indices), torch.from_numpy(S.indptr)),
+                   shape=S.shape, canonical=None)
+    M._canonical = None
+    assert distributed._rows_sorted(M)
+    i = int(np.argmax(np.diff(S.indptr) > 1))
+    a = S.indptr[i]
+    S.indices[a], S.indices[a + 1] = S.indices[a + 1], S.indices[a]
+    M2 = csr_matrix((torch.from_numpy(S.data), torch.from_numpy(S.indices), torch.from_numpy(S.indptr)),
+                    shape=S.shape, canonical=None)
+    assert not distributed._rows_sorted(M2)
