@@ -7,6 +7,9 @@
 #   seq:V1,V2,..     bit-identity digest of each variant against the others (abtest/seqcheck.py)
 #   dram5 / dram4    fabric reads split into DRAM and Infinity-Cache hits for the numeric kernel
 #                    of config 5 / 4 on the shipped library (TCC_EA0_RDREQ vs _RDREQ_DRAM)
+#   pmc4:V1,..       per-variant counter passes on config 4 (PMC4_SETS: space-separated
+#                    comma lists, one rocprofv3 --pmc pass each; a pass that rocprofv3 rejects
+#                    is reported and skipped)
 #   gputests         the whole -m gpu suite on the shipped library
 #   bench            the default bench line on the shipped library
 # usage: gpurun -- 'bash abtest/r06.sh ab4:base,d8 dram5'
@@ -30,6 +33,16 @@ for step in "$@"; do
       timeout -s KILL 240 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_DRAM_sum GRBM_GUI_ACTIVE --output-format csv -d $P -o a -- python3 $A > $P/a.log 2>&1 || { tail -5 $P/a.log; exit 1; }
       python3 profiles/summarize.py $P | grep -E "k_tile" | tee $P/summary.txt
       find $P -name "*.csv" -delete ;;
+    pmc4)
+      for v in $arg; do
+        P=gpurun_out/r06/pmc4_$v; mkdir -p $P; i=0
+        for set in ${PMC4_SETS:-SQ_WAVE_CYCLES,SQ_BUSY_CYCLES,SQ_WAIT_ANY,SQ_WAIT_INST_ANY,SQ_INSTS_VMEM_WR,SQ_INSTS_VMEM_RD,SQ_INST_CYCLES_VMEM_WR,SQ_INST_CYCLES_VMEM_RD TCP_TCC_WRITE_REQ_sum,TCP_TCC_READ_REQ_sum,TCP_PENDING_STALL_CYCLES_sum,TA_DATA_STALLED_BY_TC_CYCLES_sum,TA_ADDR_STALLED_BY_TC_CYCLES_sum,GRBM_GUI_ACTIVE}; do
+          i=$((i+1))
+          SPG_LIB=$PWD/spmm_amd/lib/libv_$v.so timeout -s KILL 90 rocprofv3 --pmc ${set//,/ } --output-format csv -d $P -o p$i -- python3 bench.py --no-config2 --no-alg3-chunked --cpu-seconds 0 --steps 1 --warmup 0 > $P/p$i.log 2>&1 || { echo "pass $i ($set) failed rc=$?"; tail -3 $P/p$i.log; }
+        done
+        echo "== $v"; python3 profiles/summarize.py $P | grep -E "k_tile_dn" | tee $P/summary.txt
+        find $P -name "*.csv" -delete
+      done ;;
     gputests)
       timeout -k 10 900 python -u -m pytest tests/ -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/r06/gpu_tests.log 2>&1; e=$?
       tail -3 gpurun_out/r06/gpu_tests.log; [ $e = 0 ] || exit 1 ;;

@@ -669,12 +669,36 @@ def run_alg3_chunked(ctx, args, tdt, n=262144, dens=1e-3, cf=0.02, steps=2, warm
     return out
 
 
+def dense_matmul_ms(torch, A, B, reps=10, warmup=3) -> float:
+    """ms per dense torch.matmul of A and B densified (same dtype, same device): the dense GEMM
+    the reference's dense_vs_sparseGEMM compares SpGEMM with, timed with events."""
+    def dense(M):
+        D = torch.zeros(M.shape, dtype=M.data.dtype, device=M.data.device)
+        rows = torch.repeat_interleave(torch.arange(M.shape[0], device=M.data.device),
+                                       (M.indptr[1:] - M.indptr[:-1]).to(torch.int64))
+        D[rows, M.indices.to(torch.int64)] = M.data
+        return D
+    Ad, Bd = dense(A), dense(B)
+    for _ in range(warmup):
+        torch.matmul(Ad, Bd)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        torch.matmul(Ad, Bd)
+    e1.record()
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    del Ad, Bd
+    return ms
+
+
 def run_config3_fp32(ctx, args, n=8192, dens=0.1, steps=10, warmup=2):
     """BASELINE config 3's densest point in fp32, the dtype of every published reference figure
     (SpGEMM_alg_comparison/profiler.py:215-222, dense_vs_sparseGEMM/utils.py:278-289): one
-    C = A.B at N=8192, density 0.1 (ALG2), with its phases.  rocBLAS sgemm on the same N takes
-    7.2 ms (profiles/r03_dense_vs_sparse_fp32.txt) -- the break-even the reference's
-    dense_vs_sparseGEMM sweep looks for."""
+    C = A.B at N=8192, density 0.1 (ALG2), with its phases, and the dense fp32 GEMM of the same
+    matrices (torch.matmul: rocBLAS/hipBLASLt sgemm) timed in the same process, as the
+    reference's dense_vs_sparseGEMM/utils.py:278-289 times its torch.matmul -- the break-even
+    that sweep looks for."""
     from spmm_amd import cusparse
     torch = ctx.torch
     A = gen_device(ctx, n, dens, args.seed, torch.float32)
@@ -687,7 +711,7 @@ def run_config3_fp32(ctx, args, n=8192, dens=0.1, steps=10, warmup=2):
     out = {"N": n, "density": dens, "dtype": "f32", "alg": 2, "num_products": int(P),
            "ms_per_step": round(elapsed / steps * 1e3, 4), "gflops": round(2.0 * P * steps / elapsed / 1e9, 3),
            "kernel": kname, "phases_ms_per_step": {k: round(v[0] / 2, 5) for k, v in ph.items() if v[1]},
-           "sgemm_ms_same_n": 7.2}
+           "sgemm_ms_same_n": round(dense_matmul_ms(torch, A, B), 4)}
     del A, B
     torch.cuda.empty_cache()
     return out

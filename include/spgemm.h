@@ -56,7 +56,7 @@ extern "C" {
 #endif
 
 #define SPG_VERSION_MAJOR 0
-#define SPG_VERSION_MINOR 1
+#define SPG_VERSION_MINOR 2
 #define SPG_VERSION_PATCH 0
 
 /* Status codes.  0..11 keep the numeric values of cusparseStatus_t so the drivers' error

@@ -46,6 +46,7 @@ struct spg_handle_s {
     // at spg_create (lds_order_check); false sends fp64 tiles to k_tile's owner rounds, which
     // need neither.  SPG_LDS_ORDERED=0 forces false (a schedule-only switch, for the tests).
     bool lds_ordered = true;
+    bool lds_ordered32 = true;      // the same for ds_add_f32 (the fp32 entry runs' third-and-later runs)
     void* scratch = nullptr;        // internal device scratch (plan-time analysis)
     size_t scratch_bytes = 0;
     // per-phase timing (spg_set_timing / spg_get_timing)
@@ -88,6 +89,7 @@ struct spg_plan_s {
     bool use_row = true;            // short rows: k_row (false: the owner-round k_short)
     bool use_tile = false;          // wide-row path: (row, column tile) items
     bool lean = true;               // fp64 tiles may use the ordered-LDS kernels (k_tile_dn / k_tile_sp)
+    bool lean32 = true;             // fp32 dense tiles may use the entry-run kernel (k_tile_dn<float>)
     int tws = 10;                   // log2 of the tile width
     int G = 1;                      // tiles per row
     int TR = 1;                     // tiles per wave task (a run of one row's tiles)
@@ -379,13 +381,13 @@ hipError_t lds_order_check_t(bool* ordered) {
     if (dout) (void)hipFree(dout);
     return e;
 }
-// both widths: ds_add_f64 (the fp64 / complex128 lean kernels) and ds_add_f32 (the fp32 runs'
-// third-and-later entries, k_tile_dn<float, ..>)
-hipError_t lds_order_check(bool* ordered) {
-    bool o64 = false, o32 = false;
-    hipError_t e = lds_order_check_t<double>(&o64);
-    if (e == hipSuccess) e = lds_order_check_t<float>(&o32);
-    *ordered = o64 && o32;
+// both widths, each its own flag: ds_add_f64 (the fp64 / complex128 lean kernels) and ds_add_f32
+// (the fp32 runs' third-and-later entries, k_tile_dn<float, ..>) -- a device failing only the
+// f32 check keeps the fp64 kernels
+hipError_t lds_order_check(bool* o64, bool* o32) {
+    *o64 = *o32 = false;
+    hipError_t e = lds_order_check_t<double>(o64);
+    if (e == hipSuccess) e = lds_order_check_t<float>(o32);
     return e;
 }
 
@@ -632,7 +634,7 @@ inline int64_t bt_entries(const spg_plan_s& p) { return p.use_tile ? rec_groups(
 #define SPG_F32_RUN_MIN 48
 #endif
 inline bool fp32_runs(const spg_plan_s& p) {
-    if (p.A.value_type != SPG_R_32F || p.B.cols <= 0 || p.B.rows <= 0 || (1 << p.tws) > 1024) return false;
+    if (!p.lean32 || p.A.value_type != SPG_R_32F || p.B.cols <= 0 || p.B.rows <= 0 || (1 << p.tws) > 1024) return false;
     const char* e = std::getenv("SPG_F32_RUNS");
     if (e && std::strcmp(e, "0") == 0) return false;
     const double seg = (double)p.B.nnz / (double)p.B.rows * (double)(1 << p.tws) / (double)p.B.cols;
@@ -1128,7 +1130,7 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
                                   (const int64_t*)tile_chunk_items(p, c), cj, cx, alpha, it_lo, it_hi, p.rgs);
         };
         if constexpr (std::is_same<T, float>::value) {
-            if (dense && p.lean && fp32_runs(p)) {   // fp32 dense tiles of long B segments: entry runs
+            if (dense && fp32_runs(p)) {   // fp32 dense tiles of long B segments: entry runs
                 hipExtLaunchKernelGGL((k_tile_dn<T, IP, 1024>), dim3(tile_grid(nit, DN_WPB)), dim3(DN_WPB * WAVE),
                                       0, h->stream, kt.a, kt.b, 0, r0, n, p.tws, p.G, Ap, Aj, Ax, p.B.rows,
                                       (const uint32_t*)p.brec, (const int32_t*)p.tptr,
@@ -1486,9 +1488,9 @@ spg_status_t spg_create(spg_handle_t* handle, int hip_device) {
     if (const char* e = std::getenv("SPG_LB_SPIN_TICKS")) h->lb_spin = std::strtoull(e, nullptr, 10);
     DeviceGuard dg_(dev);   // the handle's allocations on its device; the caller's device stays current
     hipError_t e = dg_.err;
-    if (e == hipSuccess) e = lds_order_check(&h->lds_ordered);
+    if (e == hipSuccess) e = lds_order_check(&h->lds_ordered, &h->lds_ordered32);
     if (const char* o = std::getenv("SPG_LDS_ORDERED"))
-        if (std::strcmp(o, "0") == 0) h->lds_ordered = false;
+        if (std::strcmp(o, "0") == 0) h->lds_ordered = h->lds_ordered32 = false;
     // fine-grained (coherent) host memory: the scan's system-scope stores of the scalars and
     // then the generation word become visible to the polling host in that order
     // (wait_mirror); the default host allocation is coarse-grained unless HIP_HOST_COHERENT=1
@@ -1554,6 +1556,7 @@ spg_status_t spg_plan(spg_handle_t h, const spg_csr_t* A, const spg_csr_t* B, sp
     tmp.use_short = want_short(*A, *B);
     tmp.use_row = row_kernel_enabled();
     tmp.lean = SPG_TILE_LEAN && h->lds_ordered;
+    tmp.lean32 = SPG_TILE_LEAN && h->lds_ordered32;
     tmp.use_tile = !tmp.use_short && want_tile(*A, *B, tmp.tws, tmp.G, tmp.lean);
     if (tmp.use_tile) {
         tmp.TR = 1;

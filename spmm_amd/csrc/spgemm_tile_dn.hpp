@@ -74,8 +74,21 @@ __global__ __launch_bounds__(WAVE) void k_lds_order_check(const T* __restrict__ 
 #ifndef SPG_NT_A
 #define SPG_NT_A 1
 #endif
+// SPG_NT_C: 1 non-temporal (`nt`), 0 plain, 2 agent-scope (`sc1`), 3 system-scope (`sc0 sc1`)
+// stores; A/B builds only: 4 `sc1 nt`, 5 `sc0 nt`, 6 `sc0` (vector stores in inline asm)
+#define SPG_ST_ASM(POL)                                                                               \
+    if constexpr (sizeof(T) == 8) asm volatile("global_store_dwordx2 %0, %1, off " POL ::"v"(p), "v"(v) : "memory"); \
+    else asm volatile("global_store_dword %0, %1, off " POL ::"v"(p), "v"(v) : "memory");
 template <typename T> __device__ __forceinline__ void st_c(T* p, T v) {
-    if constexpr (SPG_NT_C != 0 && (sizeof(T) == 4 || sizeof(T) == 8)) __builtin_nontemporal_store(v, p);
+    if constexpr (SPG_NT_C >= 4 && (sizeof(T) == 4 || sizeof(T) == 8)) {
+        if constexpr (SPG_NT_C == 4) { SPG_ST_ASM("sc1 nt") }
+        else if constexpr (SPG_NT_C == 5) { SPG_ST_ASM("sc0 nt") }
+        else { SPG_ST_ASM("sc0") }
+    } else if constexpr (SPG_NT_C == 2 && (sizeof(T) == 4 || sizeof(T) == 8))
+        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else if constexpr (SPG_NT_C == 3 && (sizeof(T) == 4 || sizeof(T) == 8))
+        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else if constexpr (SPG_NT_C != 0 && (sizeof(T) == 4 || sizeof(T) == 8)) __builtin_nontemporal_store(v, p);
     else *p = v;
 }
 template <typename R> __device__ __forceinline__ void st_c(cplx<R>* p, cplx<R> v) {
@@ -176,175 +189,195 @@ __device__ __forceinline__ void dn_group_markers(uint8_t* mk, int l, int cnt, in
     wsync();
 }
 
-// The ordered product walk of one item (row, tile): its A entries in batches of 64 (the first
-// NB batches' tile segments `sq` and values `aq` given, the rest loaded here); per batch a DPP
-// scan of the segment lengths and the entry table in LDS; per group of 8 chunks the transposed
-// markers; per U chunks the lane -> entry max-scans, one 16-byte table read and one record load
-// per chunk (all in flight), then per chunk in order one multiply and one ds_add_f64 into
-// acc[slot(column)] and hit(slot).  `sent` is the byte offset of the kernel's sentinel region.
-template <typename T, int NB, int MKB, typename L, typename Slot, typename Hit>
-__device__ __forceinline__ void dn_walk(L* lp, T* acc, int l, const int32_t* __restrict__ tp, int64_t a0, int nA,
-                                        T (&aq)[NB], uint2 (&sq)[NB], const int32_t* __restrict__ Aj,
-                                        const T* __restrict__ Ax, const char* __restrict__ rb, uint32_t sent,
-                                        int rgs, Slot&& slot, Hit&& hit) {
+// One batch of up to 64 A entries of the ordered walk (lane l: entry b + l, segment length
+// `cnt` at byte offset `bb` of the record array, A value `av`): the DPP scan of the segment
+// lengths and the entry table in LDS; per group of MKB chunks the transposed markers; per U
+// chunks the lane -> entry max-scans, one 16-byte table read and one record load per chunk (all
+// in flight), then per chunk in order one multiply and one ds_add_f64 into acc[slot(column)]
+// and hit(slot).  `sent` is the byte offset of the kernel's sentinel region.
+template <typename T, int MKB, typename L, typename Slot, typename Hit>
+__device__ __forceinline__ void dn_batch(L* lp, T* acc, int l, int cnt, uint32_t bb, T av, const char* __restrict__ rb,
+                                         uint32_t sent, Slot&& slot, Hit&& hit) {
     constexpr int U = (sizeof(T) > 8 ? 4 : 8) * (MKB / 8);   // chunks in flight
     constexpr int DN_MK = MKB * WAVE;                         // products per marker group
     constexpr uint32_t RB = (uint32_t)rec_bytes<T>();   // bytes of one B record
     DnEnt<T>* ent = lp->ent;
     uint8_t* mk = lp->mk;
+    const int incl = wave_incl_sum_dpp(cnt);
+    const int off = incl - cnt;
+    const int Pb = readlane_i(incl, WAVE - 1);
+    wsync();
+    ent[l].base = bb - (uint32_t)off * RB;   // wraps; base + t*RB is exact
+    ent[l].a = av;
+    if (l == 0) {
+        ent[WAVE].base = sent - (uint32_t)Pb * RB;   // products Pb.. read sentinel records
+        ent[WAVE].a = (T)0;
+    }
+    unsigned carry = 0u;
+    for (int gb = 0; gb < Pb; gb += DN_MK) {
+        dn_group_markers<MKB>(mk, l, cnt, off, gb, Pb);
+        const int nchg = min(DN_MK, Pb - gb);
+        uint64_t mrow[MKB / 8];   // this lane's marker byte of each chunk of the group
+        if constexpr (MKB == 16) {
+            const uint4 m4 = reinterpret_cast<const uint4*>(mk)[l];
+            mrow[0] = ((uint64_t)m4.y << 32) | m4.x;
+            mrow[(MKB / 8) - 1] = ((uint64_t)m4.w << 32) | m4.z;
+        } else {
+            const uint2 m2 = reinterpret_cast<const uint2*>(mk)[l];
+            mrow[0] = ((uint64_t)m2.y << 32) | m2.x;
+        }
+        for (int c0 = 0; c0 < nchg; c0 += U * WAVE) {
+            const int nu = min(U, (nchg - c0 + WAVE - 1) >> 6);
+            auto step = [&](auto nuc) {
+                constexpr int NU = decltype(nuc)::value;
+                const int cb = c0 >> 6;   // first chunk of the step (0 when U covers the group)
+                unsigned sp[NU];
+#pragma unroll
+                for (int u = 0; u < NU; ++u) {
+                    const int i = cb + u;
+                    const uint64_t w = (MKB == 16 && i >= 8) ? mrow[(MKB / 8) - 1] : mrow[0];
+                    sp[u] = wave_incl_umax_dpp((unsigned)(w >> (8 * (i & 7))) & 0xffu);
+                }
+#pragma unroll
+                for (int u = 0; u < NU; ++u) {
+                    sp[u] = max(sp[u], carry);
+                    carry = (unsigned)readlane_i((int)sp[u], WAVE - 1);
+                }
+                // product 0 of a batch always carries a marker, so sp >= 1; slots past the
+                // batch's products carry the pseudo entry's
+                int qc[NU];
+                T qv[NU], qa[NU];
+#pragma unroll
+                for (int u = 0; u < NU; ++u) {
+                    const uint32_t t = (uint32_t)(gb + c0 + u * WAVE + l);
+                    uint32_t eb;
+                    if constexpr (sizeof(T) <= 8) {   // base and value with one 16-byte read
+                        const uint4 e4 = reinterpret_cast<const uint4*>(ent)[(int)sp[u] - 1];
+                        eb = e4.x;
+                        const uint32_t w2[2] = {e4.z, e4.w};
+                        __builtin_memcpy(&qa[u], w2, sizeof(T));
+                    } else {
+                        const DnEnt<T> e = ent[(int)sp[u] - 1];
+                        eb = e.base;
+                        qa[u] = e.a;
+                    }
+                    if constexpr ((SPG_TILE_DIAG & 2) != 0) {   // timing only: no record loads
+                        qc[u] = (int)(((eb + t * 2654435761u) >> 22) & 1023u);
+                        qv[u] = (T)1;
+                    } else {
+                        load_rec_at(rb, eb + __umul24(t, RB), qc[u], qv[u]);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < NU; ++u) {
+                    const int c = slot(qc[u]);
+                    if constexpr ((SPG_TILE_DIAG & 16) != 0) {   // timing only: plain LDS stores
+                        acc[c] = mul_rn(qa[u], qv[u]);
+                    } else if constexpr ((SPG_TILE_DIAG & 32) != 0) {   // timing only: conflict-free adds
+                        lds_add(&acc[l + (c & 1)], mul_rn(qa[u], qv[u]));
+                    } else if constexpr ((SPG_TILE_DIAG & 1) == 0 && OrderedLdsAdd<T>::value) {   // (diag 1: none)
+                        lds_add(&acc[c], mul_rn(qa[u], qv[u]));   // chunk order = issue order
+                        hit(c);
+                    } else if constexpr ((SPG_TILE_DIAG & 1) == 0) {
+                        // fp32 (round 5): ds_add_f32 costs 193 CU-cycles per wave instruction on
+                        // MI355X, a plain read-add-write 17.  The products of ONE A entry in a
+                        // chunk hit distinct columns (a B row's columns are distinct), so the
+                        // chunk's run of each entry (sp[u], non-decreasing over the lanes) adds
+                        // with a plain read-add-write, runs in entry order; a chunk holding more
+                        // than two entries adds its third and later runs with one ordered
+                        // ds_add_f32 (ascending lanes = entry order).  Lanes past the batch
+                        // (pseudo entry) add nothing.
+                        const T pv = mul_rn(qa[u], qv[u]);
+                        bool live = sp[u] <= (unsigned)WAVE;
+                        // two runs whose column ranges do not overlap (a segment's tail in
+                        // high columns, the next segment's head in low ones -- most chunks
+                        // that hold a segment boundary) are distinct too: one read-add-write
+                        const unsigned long long lm = __ballot(live);   // live lanes: a prefix
+                        if (lm != 0ull) {
+                            const unsigned e0 = (unsigned)readlane_i((int)sp[u], 0);
+                            const unsigned long long m2 = __ballot(live && sp[u] != e0);
+                            bool one = m2 == 0ull;
+                            if (!one) {
+                                const int l2 = (int)__builtin_ctzll(m2), last = 63 - (int)__builtin_clzll(lm);
+                                const unsigned e1 = (unsigned)readlane_i((int)sp[u], l2);
+                                if (__ballot(live && sp[u] != e0 && sp[u] != e1) == 0ull) {
+                                    const int c1 = readlane_i(c, 0), ck = readlane_i(c, l2 - 1);
+                                    const int d1 = readlane_i(c, l2), dm = readlane_i(c, last);
+                                    one = dm < c1 || d1 > ck;
+                                }
+                            }
+                            if (one) {
+                                if (live) acc[c] = add_rn(acc[c], pv);
+                                live = false;
+                            }
+                        }
+                        for (int run = 0;; ++run) {
+                            const unsigned long long m = __ballot(live);
+                            if (m == 0ull) break;
+                            if (run == 2) {
+                                if (live) lds_add(&acc[c], pv);
+                                break;
+                            }
+                            const unsigned e0 = (unsigned)readlane_i((int)sp[u], (int)__builtin_ctzll(m));
+                            if (live && sp[u] == e0) {
+                                acc[c] = add_rn(acc[c], pv);
+                                live = false;
+                            }
+                            wsync();   // (fence + barrier: no LDS access moves across a run boundary)
+                        }
+                        hit(c);
+                    }
+                }
+            };
+            if (nu > 3 * U / 4) step(std::integral_constant<int, U>{});
+            else if (nu > U / 2) step(std::integral_constant<int, 3 * U / 4>{});
+            else if (nu > U / 4) step(std::integral_constant<int, U / 2>{});
+            else step(std::integral_constant<int, U / 4>{});
+        }
+    }
+}
+
+// Batch b's entries (the first NB batches from the register queue `sq`/`aq`, the rest loaded).
+template <typename T, int NB>
+__device__ __forceinline__ void dn_fetch(int b, int l, const int32_t* __restrict__ tp, int64_t a0, int nA, T (&aq)[NB],
+                                         uint2 (&sq)[NB], const int32_t* __restrict__ Aj, const T* __restrict__ Ax,
+                                         int rgs, int& cnt, uint32_t& bb, T& av) {
+    constexpr uint32_t RB = (uint32_t)rec_bytes<T>();
+    cnt = 0;
+    bb = 0;   // byte offset of the entry's segment in the record array
+    av = (T)0;
+    if (b < NB * WAVE) {
+        // the preloaded batches queue in registers: take the head, shift the rest down
+        // (static register indices: a select chain or a dynamic index costs more)
+        cnt = (int)(sq[0].y - sq[0].x);
+        bb = sq[0].x * RB;
+        av = aq[0];
+#pragma unroll
+        for (int q = 0; q + 1 < NB; ++q) {
+            sq[q] = sq[q + 1];
+            aq[q] = aq[q + 1];
+        }
+    } else if (b + l < nA) {
+        const uint2 se = seg_pair(tp, Aj[a0 + b + l], rgs);
+        cnt = (int)(se.y - se.x);
+        bb = se.x * RB;
+        av = Ax[a0 + b + l];
+    }
+}
+
+// The ordered product walk of one item (row, tile): its A entries in batches of 64 (the first
+// NB batches' tile segments `sq` and values `aq` given, the rest loaded here), one dn_batch each.
+template <typename T, int NB, int MKB, typename L, typename Slot, typename Hit>
+__device__ __forceinline__ void dn_walk(L* lp, T* acc, int l, const int32_t* __restrict__ tp, int64_t a0, int nA,
+                                        T (&aq)[NB], uint2 (&sq)[NB], const int32_t* __restrict__ Aj,
+                                        const T* __restrict__ Ax, const char* __restrict__ rb, uint32_t sent,
+                                        int rgs, Slot&& slot, Hit&& hit) {
     for (int b = 0; b < nA; b += WAVE) {
-        int cnt = 0;
-        uint32_t bb = 0;   // byte offset of the entry's segment in the record array
-        T av = (T)0;
-        if (b < NB * WAVE) {
-            // the preloaded batches queue in registers: take the head, shift the rest down
-            // (static register indices: a select chain or a dynamic index costs more)
-            cnt = (int)(sq[0].y - sq[0].x);
-            bb = sq[0].x * RB;
-            av = aq[0];
-#pragma unroll
-            for (int q = 0; q + 1 < NB; ++q) {
-                sq[q] = sq[q + 1];
-                aq[q] = aq[q + 1];
-            }
-        } else if (b + l < nA) {
-            const uint2 se = seg_pair(tp, Aj[a0 + b + l], rgs);
-            cnt = (int)(se.y - se.x);
-            bb = se.x * RB;
-            av = Ax[a0 + b + l];
-        }
-        const int incl = wave_incl_sum_dpp(cnt);
-        const int off = incl - cnt;
-        const int Pb = readlane_i(incl, WAVE - 1);
-        wsync();
-        ent[l].base = bb - (uint32_t)off * RB;   // wraps; base + t*RB is exact
-        ent[l].a = av;
-        if (l == 0) {
-            ent[WAVE].base = sent - (uint32_t)Pb * RB;   // products Pb.. read sentinel records
-            ent[WAVE].a = (T)0;
-        }
-        unsigned carry = 0u;
-        for (int gb = 0; gb < Pb; gb += DN_MK) {
-            dn_group_markers<MKB>(mk, l, cnt, off, gb, Pb);
-            const int nchg = min(DN_MK, Pb - gb);
-            uint64_t mrow[MKB / 8];   // this lane's marker byte of each chunk of the group
-            if constexpr (MKB == 16) {
-                const uint4 m4 = reinterpret_cast<const uint4*>(mk)[l];
-                mrow[0] = ((uint64_t)m4.y << 32) | m4.x;
-                mrow[(MKB / 8) - 1] = ((uint64_t)m4.w << 32) | m4.z;
-            } else {
-                const uint2 m2 = reinterpret_cast<const uint2*>(mk)[l];
-                mrow[0] = ((uint64_t)m2.y << 32) | m2.x;
-            }
-            for (int c0 = 0; c0 < nchg; c0 += U * WAVE) {
-                const int nu = min(U, (nchg - c0 + WAVE - 1) >> 6);
-                auto step = [&](auto nuc) {
-                    constexpr int NU = decltype(nuc)::value;
-                    const int cb = c0 >> 6;   // first chunk of the step (0 when U covers the group)
-                    unsigned sp[NU];
-#pragma unroll
-                    for (int u = 0; u < NU; ++u) {
-                        const int i = cb + u;
-                        const uint64_t w = (MKB == 16 && i >= 8) ? mrow[(MKB / 8) - 1] : mrow[0];
-                        sp[u] = wave_incl_umax_dpp((unsigned)(w >> (8 * (i & 7))) & 0xffu);
-                    }
-#pragma unroll
-                    for (int u = 0; u < NU; ++u) {
-                        sp[u] = max(sp[u], carry);
-                        carry = (unsigned)readlane_i((int)sp[u], WAVE - 1);
-                    }
-                    // product 0 of a batch always carries a marker, so sp >= 1; slots past the
-                    // batch's products carry the pseudo entry's
-                    int qc[NU];
-                    T qv[NU], qa[NU];
-#pragma unroll
-                    for (int u = 0; u < NU; ++u) {
-                        const uint32_t t = (uint32_t)(gb + c0 + u * WAVE + l);
-                        uint32_t eb;
-                        if constexpr (sizeof(T) <= 8) {   // base and value with one 16-byte read
-                            const uint4 e4 = reinterpret_cast<const uint4*>(ent)[(int)sp[u] - 1];
-                            eb = e4.x;
-                            const uint32_t w2[2] = {e4.z, e4.w};
-                            __builtin_memcpy(&qa[u], w2, sizeof(T));
-                        } else {
-                            const DnEnt<T> e = ent[(int)sp[u] - 1];
-                            eb = e.base;
-                            qa[u] = e.a;
-                        }
-                        if constexpr ((SPG_TILE_DIAG & 2) != 0) {   // timing only: no record loads
-                            qc[u] = (int)(((eb + t * 2654435761u) >> 22) & 1023u);
-                            qv[u] = (T)1;
-                        } else {
-                            load_rec_at(rb, eb + __umul24(t, RB), qc[u], qv[u]);
-                        }
-                    }
-#pragma unroll
-                    for (int u = 0; u < NU; ++u) {
-                        const int c = slot(qc[u]);
-                        if constexpr ((SPG_TILE_DIAG & 16) != 0) {   // timing only: plain LDS stores
-                            acc[c] = mul_rn(qa[u], qv[u]);
-                        } else if constexpr ((SPG_TILE_DIAG & 32) != 0) {   // timing only: conflict-free adds
-                            lds_add(&acc[l + (c & 1)], mul_rn(qa[u], qv[u]));
-                        } else if constexpr ((SPG_TILE_DIAG & 1) == 0 && OrderedLdsAdd<T>::value) {   // (diag 1: none)
-                            lds_add(&acc[c], mul_rn(qa[u], qv[u]));   // chunk order = issue order
-                            hit(c);
-                        } else if constexpr ((SPG_TILE_DIAG & 1) == 0) {
-                            // fp32 (round 5): ds_add_f32 costs 193 CU-cycles per wave instruction on
-                            // MI355X, a plain read-add-write 17.  The products of ONE A entry in a
-                            // chunk hit distinct columns (a B row's columns are distinct), so the
-                            // chunk's run of each entry (sp[u], non-decreasing over the lanes) adds
-                            // with a plain read-add-write, runs in entry order; a chunk holding more
-                            // than two entries adds its third and later runs with one ordered
-                            // ds_add_f32 (ascending lanes = entry order).  Lanes past the batch
-                            // (pseudo entry) add nothing.
-                            const T pv = mul_rn(qa[u], qv[u]);
-                            bool live = sp[u] <= (unsigned)WAVE;
-                            // two runs whose column ranges do not overlap (a segment's tail in
-                            // high columns, the next segment's head in low ones -- most chunks
-                            // that hold a segment boundary) are distinct too: one read-add-write
-                            const unsigned long long lm = __ballot(live);   // live lanes: a prefix
-                            if (lm != 0ull) {
-                                const unsigned e0 = (unsigned)readlane_i((int)sp[u], 0);
-                                const unsigned long long m2 = __ballot(live && sp[u] != e0);
-                                bool one = m2 == 0ull;
-                                if (!one) {
-                                    const int l2 = (int)__builtin_ctzll(m2), last = 63 - (int)__builtin_clzll(lm);
-                                    const unsigned e1 = (unsigned)readlane_i((int)sp[u], l2);
-                                    if (__ballot(live && sp[u] != e0 && sp[u] != e1) == 0ull) {
-                                        const int c1 = readlane_i(c, 0), ck = readlane_i(c, l2 - 1);
-                                        const int d1 = readlane_i(c, l2), dm = readlane_i(c, last);
-                                        one = dm < c1 || d1 > ck;
-                                    }
-                                }
-                                if (one) {
-                                    if (live) acc[c] = add_rn(acc[c], pv);
-                                    live = false;
-                                }
-                            }
-                            for (int run = 0;; ++run) {
-                                const unsigned long long m = __ballot(live);
-                                if (m == 0ull) break;
-                                if (run == 2) {
-                                    if (live) lds_add(&acc[c], pv);
-                                    break;
-                                }
-                                const unsigned e0 = (unsigned)readlane_i((int)sp[u], (int)__builtin_ctzll(m));
-                                if (live && sp[u] == e0) {
-                                    acc[c] = add_rn(acc[c], pv);
-                                    live = false;
-                                }
-                                __builtin_amdgcn_wave_barrier();
-                            }
-                            hit(c);
-                        }
-                    }
-                };
-                if (nu > 3 * U / 4) step(std::integral_constant<int, U>{});
-                else if (nu > U / 2) step(std::integral_constant<int, 3 * U / 4>{});
-                else if (nu > U / 4) step(std::integral_constant<int, U / 2>{});
-                else step(std::integral_constant<int, U / 4>{});
-            }
-        }
+        int cnt;
+        uint32_t bb;
+        T av;
+        dn_fetch<T, NB>(b, l, tp, a0, nA, aq, sq, Aj, Ax, rgs, cnt, bb, av);
+        dn_batch<T, MKB>(lp, acc, l, cnt, bb, av, rb, sent, slot, hit);
     }
 }
 
@@ -354,8 +387,13 @@ template <typename T, int TWD>
 __device__ __forceinline__ void dn_emit(DnLds<T, TWD>& S, int l, int TW, int lo, int nnz, const int32_t* __restrict__ tp,
                                         int64_t a0, int nA, const int32_t* __restrict__ Aj,
                                         const char* __restrict__ rb, int32_t* __restrict__ crow,
-                                        T* __restrict__ xrow, T alpha, int rgs) {
+                                        T* __restrict__ xrow, T alpha, int rgs, int32_t* cj0 = nullptr,
+                                        T* cx0 = nullptr) {
     constexpr uint32_t RB = (uint32_t)rec_bytes<T>();
+    // (diag 1024, timing only: every store full and aligned, into a per-wave 64-entry region of C)
+    const uint32_t wreg = ((blockIdx.x * DN_WPB + (threadIdx.x >> 6)) & 4095u) * 64u;
+    int32_t* crow_al = cj0 + wreg;
+    T* xrow_al = cx0 + wreg;
     wsync();
     // the item's structure, 64 columns at a time: hit[] or (dn_sent) the non -0.0 slots
     // (4 column groups per round: their LDS reads in flight together, TW >= 256)
@@ -374,7 +412,10 @@ __device__ __forceinline__ void dn_emit(DnLds<T, TWD>& S, int l, int TW, int lo,
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const unsigned long long m = __ballot(h[e]);
-                if (h[e] && (SPG_TILE_DIAG & 8) == 0) {   // (diag 8, timing only: no output)
+                if constexpr ((SPG_TILE_DIAG & 1024) != 0) {   // (diag 1024: full aligned 64-lane stores)
+                    st_c(crow_al + l, (int32_t)(lo + (k0 + e) * WAVE + l));
+                    st_c(xrow_al + l, v[e]);
+                } else if (h[e] && (SPG_TILE_DIAG & 8) == 0) {   // (diag 8, timing only: no output)
                     uint32_t p = (uint32_t)(run + lane_rank(m));
                     if constexpr ((SPG_TILE_DIAG & 128) != 0) p &= 63u;   // (diag 128: the same stores, L2-resident)
                     st_c(crow + p, (int32_t)(lo + (k0 + e) * WAVE + l));
@@ -434,13 +475,13 @@ __device__ __forceinline__ void dn_item(DnLds<T, TWD>& S, int l, int TW, int lo,
                                         const int32_t* __restrict__ Aj,
                                         const T* __restrict__ Ax, const char* __restrict__ rb, uint32_t sent,
                                         int32_t* __restrict__ crow,
-                                        T* __restrict__ xrow, T alpha, int rgs) {
+                                        T* __restrict__ xrow, T alpha, int rgs, int32_t* cj0, T* cx0) {
     dn_clear(S, l, TW);
     dn_walk<T, NB, dn_mkb(TWD)>(&S, S.acc, l, tp, a0, nA, aq, sq, Aj, Ax, rb, sent, rgs, [&](int c) { return c; },
                    [&](int c) {
                        if constexpr (!dn_sent<T>()) S.hit[c] = 1;
                    });
-    dn_emit<T, TWD>(S, l, TW, lo, nnz, tp, a0, nA, Aj, rb, crow, xrow, alpha, rgs);
+    dn_emit<T, TWD>(S, l, TW, lo, nnz, tp, a0, nA, Aj, rb, crow, xrow, alpha, rgs, cj0, cx0);
 }
 // Numeric pass on dense tiles: one wave per (row, tile) item, items tile-major over the
 // XCD-aware block map (an XCD works through one tile at a time, so the tile's B slice and
@@ -500,7 +541,7 @@ __global__ __launch_bounds__(DN_WPB * WAVE) void k_tile_dn(
 #pragma unroll
         for (int q = 0; q < NB; ++q) sq[q] = kq[q] >= 0 ? seg_pair(tp, kq[q], rgs) : make_uint2(0u, 0u);
         dn_item<T, NB, TWD>(S, l, TW, g * TW, nnz, tp, a0, nA, aq, sq, Aj, Ax, rb, sent, Cj + obase, Cx + obase, alpha,
-                            rgs);
+                            rgs, Cj, Cx);
     }
 }
 

@@ -44,7 +44,7 @@ def test_python_binding_prototypes_cover_header():
 def test_library_loads_without_gpu():
     from spmm_amd import _lib
     lib = _lib.load()
-    assert lib.spg_version() == 100
+    assert lib.spg_version() == 200   # 0.2.0: spg_plan_info_t.record_group, 9 timing phases (round 5)
     for code, name in _lib.STATUS_NAMES.items():
         assert lib.spg_status_string(code).decode() == name
     # no device in this container: creating a handle must fail with a status, not crash

@@ -49,13 +49,29 @@ def _full_bitexact(Ah, Bh, alg, cf=0.2, threads=0):
     return C
 
 
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("density", [1e-2, 1e-1])
-def test_config3_full_bitexact(density):
+def test_config3_full_bitexact(density, dtype):
+    """fp32 at density 0.1 is bench.py's `config3_fp32` point (the fp32 entry-run kernel)."""
     from spmm_amd import gen
-    Ah, Bh = gen.scipy_pair(8192, density, seed=42)
+    Ah, Bh = gen.scipy_pair(8192, density, seed=42, dtype=dtype)
     C = _full_bitexact(Ah, Bh, alg=2, threads=THREADS if density >= 0.1 else 0)
     if density >= 0.1:
         assert C.nnz == 8192 * 8192   # every entry of C is reached at density 0.1
+
+
+def test_config3_fp32_bench_matrices_bitexact():
+    """The exact matrices of bench.py's `config3_fp32` key (gen.random_csr on the device, seeds
+    42 and 43, fp32, N = 8192, density 0.1): every row bit-exact against the OpenMP oracle."""
+    from spmm_amd import cusparse, gen
+    A = gen.random_csr(8192, 8192, 0.1, seed=42, dtype=torch.float32, device=DEV)
+    B = gen.random_csr(8192, 8192, 0.1, seed=43, dtype=torch.float32, device=DEV)
+    C = cusparse.spgemm(A, B, alg=2)
+    torch.cuda.synchronize()
+    rp, rj, rx = oracle.spgemm(A.get(), B.get(), keep_zeros=True, sort=True, threads=THREADS)
+    assert np.array_equal(C.indptr.cpu().numpy().astype(np.int64), rp)
+    assert np.array_equal(C.indices.cpu().numpy(), rj)
+    assert np.array_equal(_bits(C.data.cpu().numpy()), _bits(rx))
 
 
 def _expected_nnz(a_lens, n, density):
