@@ -10,6 +10,8 @@
 #   pmc4:V1,..       per-variant counter passes on config 4 (PMC4_SETS: space-separated
 #                    comma lists, one rocprofv3 --pmc pass each; a pass that rocprofv3 rejects
 #                    is reported and skipped)
+#   f32:V1,..        fp32 products (F32_SHAPES "N:density ..."): bench phases per variant
+#   ptest:V:EXPR     pytest -m gpu -k EXPR against variant V's library (SPG_LIB; EXPR all: no -k)
 #   gputests         the whole -m gpu suite on the shipped library
 #   bench            the default bench line on the shipped library
 # usage: gpurun -- 'bash abtest/r06.sh ab4:base,d8 dram5'
@@ -43,6 +45,18 @@ for step in "$@"; do
         echo "== $v"; python3 profiles/summarize.py $P | grep -E "k_tile_dn" | tee $P/summary.txt
         find $P -name "*.csv" -delete
       done ;;
+    f32)
+      for sh in ${F32_SHAPES:-65536:0.005 16384:0.01 8192:0.01 8192:0.1}; do
+        n=${sh%%:*}; d=${sh#*:}
+        for v in $arg; do
+          SPG_LIB=$PWD/spmm_amd/lib/libv_$v.so timeout -k 10 300 python bench.py --no-config2 --no-alg3-chunked --cpu-seconds 0 --dtype float32 --alg 2 --n $n --density $d --steps 5 --warmup 2 > gpurun_out/r06/f32_${v}_${n}_${d}.json 2> gpurun_out/r06/f32_${v}_${n}_${d}.err || { echo "f32 $v $n $d failed"; tail -3 gpurun_out/r06/f32_${v}_${n}_${d}.err; exit 1; }
+          python3 -c "import json; d=json.load(open('gpurun_out/r06/f32_${v}_${n}_${d}.json')); print('$v $n $d', d['value'], d['ms_per_step'], d['phases_ms_per_step'])"
+        done
+      done ;;
+    ptest)
+      v=${arg%% *}; k=${arg#* }; K=(-k "$k"); [ "$k" = all ] && K=()
+      SPG_LIB=$PWD/spmm_amd/lib/libv_$v.so timeout -k 10 900 python -u -m pytest tests/ -x -q -m gpu "${K[@]}" --timeout 300 --timeout-method thread > gpurun_out/r06/ptest_$v.log 2>&1; e=$?
+      tail -3 gpurun_out/r06/ptest_$v.log; [ $e = 0 ] || exit 1 ;;
     gputests)
       timeout -k 10 900 python -u -m pytest tests/ -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/r06/gpu_tests.log 2>&1; e=$?
       tail -3 gpurun_out/r06/gpu_tests.log; [ $e = 0 ] || exit 1 ;;
