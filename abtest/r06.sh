@@ -54,7 +54,7 @@ for step in "$@"; do
         done
       done ;;
     ptest)
-      v=${arg%% *}; k=${arg#* }; K=(-k "$k"); [ "$k" = all ] && K=()
+      v=${arg%%:*}; k=${arg#*:}; K=(-k "$k"); [ "$k" = all ] && K=(-m gpu)
       SPG_LIB=$PWD/spmm_amd/lib/libv_$v.so timeout -k 10 900 python -u -m pytest tests/ -x -q -m gpu "${K[@]}" --timeout 300 --timeout-method thread > gpurun_out/r06/ptest_$v.log 2>&1; e=$?
       tail -3 gpurun_out/r06/ptest_$v.log; [ $e = 0 ] || exit 1 ;;
     gputests)

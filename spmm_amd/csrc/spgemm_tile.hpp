@@ -678,6 +678,14 @@ __global__ __launch_bounds__(TILE_WPB * WAVE) __attribute__((amdgpu_waves_per_eu
     }
 }
 
+// SPG_SYM8_PF (round 6): k_tile_sym8c loads the next batch's extents during the current batch
+// (config 5 symbolic 12.0 -> 11.5 ms; 0: round 5's per-batch dependent chain)
+#ifndef SPG_SYM8_PF
+#define SPG_SYM8_PF 1
+#endif
+#ifndef SPG_SYM8_U
+#define SPG_SYM8_U 8   // (A/B: chunks of 64 words in flight in k_tile_sym8c)
+#endif
 // k_tile_sym8 with CW waves per task (round 5): the task's bitmap is shared in LDS by the
 // block's waves (the bitmap OR is order-free: ds_or from any wave), each wave walks every CW-th
 // batch of 64 A entries with its own entry table and markers.  The 8 KB bitmap is then paid once
@@ -696,7 +704,7 @@ __global__ __launch_bounds__(CW * WAVE) void k_tile_sym8c(
     int64_t row0, int64_t nrows, int tws, int G, int twss, const IP* __restrict__ Ap,
     const int32_t* __restrict__ Aj, const IP* __restrict__ Bp, const uint16_t* __restrict__ Bj16,
     const uint32_t* __restrict__ sidx, uint32_t* __restrict__ bitmap, int64_t* __restrict__ item_cnt) {
-    constexpr int U = 8;   // chunks of 64 words in flight
+    constexpr int U = SPG_SYM8_U;   // chunks of 64 words in flight
     constexpr int NT = CW * WAVE;
     __shared__ __attribute__((aligned(16))) Sym8Blk<CW> blk;
     const int l = lane_id();
@@ -724,76 +732,112 @@ __global__ __launch_bounds__(CW * WAVE) void k_tile_sym8c(
         }
         for (int w = tid; w < nws; w += NT) bits[w] = 0u;
         __syncthreads();
-        for (int b = wv * WAVE; b < nA; b += NT) {
-            int wlen = 0;
-            Sym8Ent e{0u, 0u, 0u, 0u};
-            int64_t bg = 0;
-            int cnt = 0;
-            if (b + l < nA) {
-                const int32_t k = Aj[a0 + b + l];
-                const IP rb = Bp[k];
-                if (Gs == 1) {
-                    cnt = (int)(Bp[k + 1] - rb);
-                    bg = (int64_t)rb;
+        // SPG_SYM8_PF (round 6): the next batch's extents (A column -> B row start and, for a
+        // row cut into symbolic tiles, the tile's bounds) are loaded during this batch, as raw
+        // words (unconditional loads at a clamped entry; nothing waits for them until the next
+        // batch starts) -- one dependent chain of three loads per batch no longer stalls it
+        // (specialised for whole-row symbolic tiles, Gs == 1: no uniform branch between a load
+        // and its use)
+        auto batches = [&](auto gs1) {
+            IP xr = 0, xe = 0;
+            uint32_t xs0 = 0u, xs1 = 0u;
+            auto fetch = [&](int bn) {
+                const int32_t k = Aj[a0 + min(bn + l, nA - 1)];
+                xr = Bp[k];
+                if constexpr (decltype(gs1)::value) {
+                    xe = Bp[k + 1];
                 } else {
                     const uint32_t* sk = sidx + (int64_t)k * (Gs + 1);
-                    const uint32_t s0 = sk[gs];
-                    cnt = (int)(sk[gs + 1] - s0);
-                    bg = (int64_t)rb + s0;
+                    xs0 = sk[gs];
+                    xs1 = sk[gs + 1];
                 }
-            }
-            if (cnt > 0) {
-                wlen = (int)(((bg + cnt + 7) >> 3) - (bg >> 3));
-                e.w0 = (uint32_t)(bg >> 3);
-                e.lohi = (uint32_t)(bg & 7) | ((uint32_t)(((bg + cnt - 1) & 7) + 1) << 8);
-            }
-            const int incl = wave_incl_sum_dpp(wlen);
-            const int woff = incl - wlen;
-            const int Wb = readlane_i(incl, WAVE - 1);
-            wsync();
-            e.woff = (uint32_t)woff;
-            e.wlen = (uint32_t)wlen;
-            S.ent[l] = e;
-            wsync();
-            unsigned carry = 0u;
-            for (int gb = 0; gb < Wb; gb += TILE_MK) {
-                group_markers(S, l, wlen, woff, gb);
-                const int nchg = min(TILE_MK, Wb - gb);
-                const uint4 mrow = reinterpret_cast<const uint4*>(S.mk)[l];
-                for (int c0 = 0; c0 < nchg; c0 += U * WAVE) {
-                    const uint64_t mb = marker_bytes(mrow, c0 >> 6);
-                    uint4 w[U];
-                    uint32_t lo[U], hi[U];
-#pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        lo[u] = 8u;   // (no valid column: slots past the group's words)
-                        hi[u] = 0u;
-                        w[u] = make_uint4(0u, 0u, 0u, 0u);
-                        const int cc = c0 + u * WAVE;
-                        if (cc < nchg) {
-                            const unsigned sp = max(wave_incl_umax_dpp((unsigned)(mb >> (8 * u)) & 0xffu), carry);
-                            carry = (unsigned)readlane_i((int)sp, WAVE - 1);
-                            const int t = gb + cc + l;
-                            if (t < Wb) {
-                                const Sym8Ent x = S.ent[(int)sp - 1];
-                                const uint32_t wi = (uint32_t)t - x.woff;
-                                lo[u] = wi == 0u ? (x.lohi & 0xffu) : 0u;
-                                hi[u] = wi + 1u == x.wlen ? (x.lohi >> 8) : 8u;
-                                w[u] = W[x.w0 + wi];
-                            }
+            };
+            if (SPG_SYM8_PF) fetch(wv * WAVE);
+            for (int b = wv * WAVE; b < nA; b += NT) {
+                int wlen = 0;
+                Sym8Ent e{0u, 0u, 0u, 0u};
+                int64_t bg = 0;
+                int cnt = 0;
+                if (SPG_SYM8_PF) {
+                    if (b + l < nA) {
+                        if constexpr (decltype(gs1)::value) {
+                            cnt = (int)(xe - xr);
+                            bg = (int64_t)xr;
+                        } else {
+                            cnt = (int)(xs1 - xs0);
+                            bg = (int64_t)xr + xs0;
                         }
                     }
+                    fetch(b + NT);   // (unconditional: a conditional load would make the compiler wait for it)
+                } else if (b + l < nA) {
+                    const int32_t k = Aj[a0 + b + l];
+                    const IP rb = Bp[k];
+                    if (Gs == 1) {
+                        cnt = (int)(Bp[k + 1] - rb);
+                        bg = (int64_t)rb;
+                    } else {
+                        const uint32_t* sk = sidx + (int64_t)k * (Gs + 1);
+                        const uint32_t s0 = sk[gs];
+                        cnt = (int)(sk[gs + 1] - s0);
+                        bg = (int64_t)rb + s0;
+                    }
+                }
+                if (cnt > 0) {
+                    wlen = (int)(((bg + cnt + 7) >> 3) - (bg >> 3));
+                    e.w0 = (uint32_t)(bg >> 3);
+                    e.lohi = (uint32_t)(bg & 7) | ((uint32_t)(((bg + cnt - 1) & 7) + 1) << 8);
+                }
+                const int incl = wave_incl_sum_dpp(wlen);
+                const int woff = incl - wlen;
+                const int Wb = readlane_i(incl, WAVE - 1);
+                wsync();
+                e.woff = (uint32_t)woff;
+                e.wlen = (uint32_t)wlen;
+                S.ent[l] = e;
+                wsync();
+                unsigned carry = 0u;
+                for (int gb = 0; gb < Wb; gb += TILE_MK) {
+                    group_markers(S, l, wlen, woff, gb);
+                    const int nchg = min(TILE_MK, Wb - gb);
+                    const uint4 mrow = reinterpret_cast<const uint4*>(S.mk)[l];
+                    for (int c0 = 0; c0 < nchg; c0 += U * WAVE) {
+                        const uint64_t mb = marker_bytes(mrow, c0 >> 6);
+                        const uint64_t mb2 = U > 8 ? marker_bytes(mrow, (c0 >> 6) + 8) : 0ull;   // (chunks 8..15 of a 16-chunk step)
+                        uint4 w[U];
+                        uint32_t lo[U], hi[U];
 #pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        const uint32_t ww[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
+                        for (int u = 0; u < U; ++u) {
+                            lo[u] = 8u;   // (no valid column: slots past the group's words)
+                            hi[u] = 0u;
+                            w[u] = make_uint4(0u, 0u, 0u, 0u);
+                            const int cc = c0 + u * WAVE;
+                            if (cc < nchg) {
+                                const unsigned sp = max(wave_incl_umax_dpp((unsigned)((u < 8 ? mb : mb2) >> (8 * (u & 7))) & 0xffu), carry);
+                                carry = (unsigned)readlane_i((int)sp, WAVE - 1);
+                                const int t = gb + cc + l;
+                                if (t < Wb) {
+                                    const Sym8Ent x = S.ent[(int)sp - 1];
+                                    const uint32_t wi = (uint32_t)t - x.woff;
+                                    lo[u] = wi == 0u ? (x.lohi & 0xffu) : 0u;
+                                    hi[u] = wi + 1u == x.wlen ? (x.lohi >> 8) : 8u;
+                                    w[u] = W[x.w0 + wi];
+                                }
+                            }
+                        }
 #pragma unroll
-                        for (int h = 0; h < 8; ++h)
-                            if ((uint32_t)h >= lo[u] && (uint32_t)h < hi[u])
-                                set_bit(bits, (int)((ww[h >> 1] >> (16 * (h & 1))) & 0xffffu) - lo16);
+                        for (int u = 0; u < U; ++u) {
+                            const uint32_t ww[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
+#pragma unroll
+                            for (int h = 0; h < 8; ++h)
+                                if ((uint32_t)h >= lo[u] && (uint32_t)h < hi[u])
+                                    set_bit(bits, (int)((ww[h >> 1] >> (16 * (h & 1))) & 0xffffu) - lo16);
+                        }
                     }
                 }
             }
-        }
+        };
+        if (Gs == 1) batches(std::true_type{});
+        else batches(std::false_type{});
         __syncthreads();
         if (bitmap) {   // (dense numeric tiles take their structure from the accumulation)
             uint32_t* __restrict__ out = bitmap + ((row - row0) * G + t0) * (int64_t)nw;

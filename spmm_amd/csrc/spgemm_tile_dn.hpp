@@ -775,6 +775,14 @@ void k_tile_sp(
 // k_tile_sym.  (Measured on config 4: 4.05 ms against 7.05 ms for k_tile_sym's flattened
 // walk over 16384-column tiles and 7.0 ms for a one-entry-per-instruction cursor walk.)
 constexpr int SEG_WPB = 2;
+#ifndef SPG_SYM_NQ
+#define SPG_SYM_NQ 4   // (A/B: quads of A entries per round of k_tile_sym_seg)
+#endif
+// SPG_SYM_PF (round 6): the first SPG_SYM_PF steps of a k_tile_sym_seg round load together, with
+// the next round's extents loaded under them (config 4 symbolic 2.74 -> 2.51 ms; 0: round 5's loop)
+#ifndef SPG_SYM_PF
+#define SPG_SYM_PF 3
+#endif
 // `ncols` > 0 (plans whose C rows are expected to be full, SPG_SYM_FULL in spgemm.hip): every 64
 // A entries the wave counts its bitmap, and a task whose columns [lo, min(lo + width, ncols))
 // are all set stops walking -- later products cannot add a column (config 3 at density 0.1:
@@ -785,7 +793,7 @@ __global__ __launch_bounds__(SEG_WPB * WAVE) void k_tile_sym_seg(
     const int32_t* __restrict__ Aj, const IP* __restrict__ Bp, const uint16_t* __restrict__ Bj16,
     const uint32_t* __restrict__ sidx, uint32_t* __restrict__ bitmap, int64_t* __restrict__ item_cnt,
     int64_t ncols) {
-    constexpr int NQ = 4;   // quads of A entries per round: 16 entries, 4 loads in flight per lane
+    constexpr int NQ = SPG_SYM_NQ;   // quads of A entries per round: 16 entries, 4 loads in flight per lane
     __shared__ __attribute__((aligned(16))) uint32_t bits_all[SEG_WPB][SYM_NWMAX];
     const int l = lane_id();
     const int sub = l & 15, grp = l >> 4;
@@ -840,53 +848,116 @@ __global__ __launch_bounds__(SEG_WPB * WAVE) void k_tile_sym_seg(
         extents(0, cnt, beg);
         // the task's valid columns (the last tile of a row may pass the matrix's last column)
         const int full = ncols > 0 ? (int)min((int64_t)nws * 32, ncols - ((int64_t)t0 << tws)) : 0;
-        for (int b = 0; b < nA; b += 4 * NQ) {
-            if (full > 0 && b > 0 && (b & (WAVE - 1)) == 0) {   // every 64 entries: full yet?
-                wsync();
-                int c = 0;
-                for (int w = l; w < nws; w += WAVE) c += __popc(bits[w]);
-                c = wave_incl_sum_dpp(c);
-                if (readlane_i(c, WAVE - 1) >= full) break;
-            }
-            // eight 16-bit columns per lane per 16-byte load: each segment from its 8-aligned
-            // start (span = cnt + (beg & 7) elements; an element before beg or past the segment
-            // is skipped; the region is padded, so the last load stays inside it).  A 16-lane
-            // group covers 128 columns per step; the longest span of the round sets the steps.
-            int odd[NQ], span[NQ];
-            const uint4* __restrict__ w0[NQ];
-            int mx = 0;
+        // one round: NQ quads of A entries; eight 16-bit columns per lane per 16-byte load, each
+        // segment from its 8-aligned start (span = cnt + (beg & 7) elements; an element before
+        // beg or past the segment is skipped; the region is padded, so the last load stays
+        // inside it).  A 16-lane group covers 128 columns per step; the longest span of the
+        // round sets the steps.
+        int odd[NQ], span[NQ];
+        const uint4* __restrict__ w0[NQ];
+        auto or_step = [&](int e, const uint4 (&w)[NQ]) {
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
-                odd[q] = (int)(beg[q] & 7);
-                span[q] = cnt[q] + odd[q];
-                w0[q] = reinterpret_cast<const uint4*>(Bj16 + (beg[q] - odd[q]));
-                mx = max(mx, span[q]);
-            }
-            mx = max(mx, __shfl_xor(mx, 16, WAVE));
-            mx = max(mx, __shfl_xor(mx, 32, WAVE));
-            mx = uniform(mx);
-            for (int e = 0; e < mx; e += 128) {
-                uint4 w[NQ];
+                const int x = e + 8 * sub;
+                const uint32_t ww[4] = {w[q].x, w[q].y, w[q].z, w[q].w};
 #pragma unroll
-                for (int q = 0; q < NQ; ++q) {
-                    const int x = e + 8 * sub;
-                    w[q] = x < span[q] ? w0[q][x >> 3] : make_uint4(0u, 0u, 0u, 0u);
+                for (int h = 0; h < 8; ++h) {
+                    const int xh = x + h;
+                    if (xh >= odd[q] && xh < span[q])
+                        set_bit(bits, (int)((ww[h >> 1] >> (16 * (h & 1))) & 0xffffu) - lo16);
                 }
-                if (e == 0) extents(b + 4 * NQ, cnt, beg);   // (next round; span/odd/w0 are kept)
+            }
+        };
+        // (the loop is specialised for whole-row symbolic tiles, Gs == 1, so no uniform branch on
+        // it sits between a load and its use)
+        auto rounds = [&](auto gs1) {
+            IP xr0[NQ], xr1[NQ];       // (SPG_SYM_PF: the next round's B row starts / ends,
+            uint32_t xs0[NQ], xs1[NQ];  // or its symbolic-tile bounds, as loaded)
+            bool pend = false;
+            for (int b = 0; b < nA; b += 4 * NQ) {
+                if (full > 0 && b > 0 && (b & (WAVE - 1)) == 0) {   // every 64 entries: full yet?
+                    wsync();
+                    int c = 0;
+                    for (int w = l; w < nws; w += WAVE) c += __popc(bits[w]);
+                    c = wave_incl_sum_dpp(c);
+                    if (readlane_i(c, WAVE - 1) >= full) break;
+                }
+                if (SPG_SYM_PF > 0 && pend) {   // this round's extents from the raw words loaded last round
 #pragma unroll
-                for (int q = 0; q < NQ; ++q) {
-                    const int x = e + 8 * sub;
-                    const uint32_t ww[4] = {w[q].x, w[q].y, w[q].z, w[q].w};
-#pragma unroll
-                    for (int h = 0; h < 8; ++h) {
-                        const int xh = x + h;
-                        if (xh >= odd[q] && xh < span[q])
-                            set_bit(bits, (int)((ww[h >> 1] >> (16 * (h & 1))) & 0xffffu) - lo16);
+                    for (int q = 0; q < NQ; ++q) {
+                        const bool ok = b + 4 * q + grp < nA;
+                        if constexpr (decltype(gs1)::value) {
+                            cnt[q] = ok ? (int)(xr1[q] - xr0[q]) : 0;
+                            beg[q] = ok ? (int64_t)xr0[q] : 0;
+                        } else {
+                            cnt[q] = ok ? (int)(xs1[q] - xs0[q]) : 0;
+                            beg[q] = ok ? (int64_t)xr0[q] + xs0[q] : 0;
+                        }
                     }
                 }
+                int mx = 0;
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    odd[q] = (int)(beg[q] & 7);
+                    span[q] = cnt[q] + odd[q];
+                    w0[q] = reinterpret_cast<const uint4*>(Bj16 + (beg[q] - odd[q]));
+                    mx = max(mx, span[q]);
+                }
+                mx = max(mx, __shfl_xor(mx, 16, WAVE));
+                mx = max(mx, __shfl_xor(mx, 32, WAVE));
+                mx = uniform(mx);
+                int e0 = 0;
+                if constexpr (SPG_SYM_PF > 0) {
+                    // round 6: the next round's A columns first, then this round's first SPG_SYM_PF
+                    // steps of column loads (unconditional: an index past the segment re-reads its
+                    // last 16 bytes and is masked), then the next round's B extents (waiting only for
+                    // the A columns: the column loads stay in flight), then the ORs: about one memory
+                    // round trip per round instead of one per step plus a dependent chain per quad
+                    int32_t kn[NQ];
+#pragma unroll
+                    for (int q = 0; q < NQ; ++q) kn[q] = Aj[a0 + min(b + 4 * NQ + 4 * q + grp, nA - 1)];
+                    uint4 w[SPG_SYM_PF > 0 ? SPG_SYM_PF : 1][NQ];
+#pragma unroll
+                    for (int st = 0; st < SPG_SYM_PF; ++st)
+#pragma unroll
+                        for (int q = 0; q < NQ; ++q) {
+                            const int last = max(span[q] - 1, 0) >> 3;
+                            w[st][q] = w0[q][min((st * 128 + 8 * sub) >> 3, last)];
+                        }
+                    // (raw words only: they are combined at the next round's start, so nothing waits
+                    // for them before the ORs)
+#pragma unroll
+                    for (int q = 0; q < NQ; ++q) {
+                        xr0[q] = Bp[kn[q]];
+                        if constexpr (decltype(gs1)::value) {
+                            xr1[q] = Bp[kn[q] + 1];
+                        } else {
+                            const uint32_t* sk = sidx + (int64_t)kn[q] * (Gs + 1);
+                            xs0[q] = sk[gs];
+                            xs1[q] = sk[gs + 1];
+                        }
+                    }
+                    pend = true;
+#pragma unroll
+                    for (int st = 0; st < SPG_SYM_PF; ++st)
+                        if (st * 128 < mx) or_step(st * 128, w[st]);
+                    e0 = SPG_SYM_PF * 128;
+                }
+                for (int e = e0; e < mx; e += 128) {
+                    uint4 w[NQ];
+#pragma unroll
+                    for (int q = 0; q < NQ; ++q) {
+                        const int x = e + 8 * sub;
+                        w[q] = x < span[q] ? w0[q][x >> 3] : make_uint4(0u, 0u, 0u, 0u);
+                    }
+                    if (SPG_SYM_PF == 0 && e == 0) extents(b + 4 * NQ, cnt, beg);   // (next round; span/odd/w0 are kept)
+                    or_step(e, w);
+                }
+                if (SPG_SYM_PF == 0 && mx == 0) extents(b + 4 * NQ, cnt, beg);
             }
-            if (mx == 0) extents(b + 4 * NQ, cnt, beg);
-        }
+        };
+        if (Gs == 1) rounds(std::true_type{});
+        else rounds(std::false_type{});
         wsync();
         if (bitmap) {
             uint32_t* __restrict__ out = bitmap + ((row - row0) * G + t0) * (int64_t)nw;
