@@ -245,7 +245,7 @@ inline bool want_tile(const spg_csr_t& A, const spg_csr_t& B, int& tws, int& G, 
     // fp64 C rows at least half dense and wide: dense tiles of 2048 columns (a 2048-slot
     // accumulator).  Half the items, half the segment-table lookups per product; config 4
     // measured 24.9 against 26.6 ms per product with 1024-column tiles.
-    if (B.value_type == SPG_R_64F && lean && tws == 10 && frac >= 0.5 && B.cols >= 16384) tws = 11;
+    if (B.value_type == SPG_R_64F && lean && tws == 10 && frac >= 0.5 && B.cols >= 16384) tws = SPG_DN_WIDE_TWS;
     // fp64 C rows 10-24 % dense over >= 16384 columns: sparse tiles of 8192 columns (2048-slot
     // windows; half the items, A-row reads and segment-table lookups of 4096-column tiles;
     // config 5: 149.3 -> 124.8 ms per product)
@@ -1202,6 +1202,13 @@ spg_status_t tile_numeric(spg_handle_t h, spg_plan_s& p, int32_t* cj, T* cx, T a
                                           sent(sentinel_region(TWD)), it_lo, it_hi, p.rgs);
                 };
                 if constexpr (std::is_same<T, double>::value) {
+                    if constexpr (DN_TW_MAX > 2048) {
+                        if ((1 << p.tws) > 2048) {
+                            dn(std::integral_constant<int, DN_TW_MAX>{});
+                            SPG_LAUNCHED(h);
+                            continue;
+                        }
+                    }
                     if ((1 << p.tws) > 1024) dn(std::integral_constant<int, 2048>{});
                     else dn(std::integral_constant<int, 1024>{});
                 } else {

@@ -265,18 +265,25 @@ __device__ __forceinline__ void store_rec_val(uint32_t* __restrict__ rec, int64_
 
 // Sentinel records after B's nnz records: the lean tile kernels point every product slot past
 // the end of a batch at them instead of masking the slot (no compare / select per chunk).
-// Regions 0 and 1 (dense tiles of 1024 / 2048 columns): columns 1024 / 2048 + (i % 32),
+// Regions 0, 1 and 3 (dense tiles of 1024 / 2048 / 4096 columns): columns 1024 / 2048 / 4096 + (i % 32),
 // accumulator slots nobody reads; region 2 (sparse tiles, <= 8192 columns): columns
 // 65472 + (i % 64), outside every window (and within the 10-byte records' u16).  Value 0.
 constexpr int SENT_N = 512;        // records per region: a step never runs more than 512 slots past its batch
-constexpr int SENT_REGIONS = 3;
+constexpr int SENT_REGIONS = 4;
 constexpr int DN_DUMMY = 32;       // accumulator slots past a dense tile: the sentinel records add into them
-constexpr int DN_TW_MAX = 2048;    // widest dense tile (fp64: 2048-slot accumulator)
+// SPG_DN_WIDE_TWS: log2 of the widest fp64 dense tile (11: 2048 columns; 12: 4096, A/B builds)
+#ifndef SPG_DN_WIDE_TWS
+#define SPG_DN_WIDE_TWS 11
+#endif
+constexpr int DN_TW_MAX = 1 << SPG_DN_WIDE_TWS;   // widest dense tile (fp64: its accumulator's slots)
 __device__ __forceinline__ int sentinel_col(int i) {
     const int r = i / SENT_N, x = i % SENT_N;
-    return r == 0 ? 1024 + (x & (DN_DUMMY - 1)) : r == 1 ? 2048 + (x & (DN_DUMMY - 1)) : 0xffc0 + (x & 63);
+    return r == 0 ? 1024 + (x & (DN_DUMMY - 1)) : r == 1 ? 2048 + (x & (DN_DUMMY - 1))
+                                                : r == 3 ? 4096 + (x & (DN_DUMMY - 1)) : 0xffc0 + (x & 63);
 }
-__host__ __device__ constexpr int sentinel_region(int dense_tw) { return dense_tw == 1024 ? 0 : dense_tw == 2048 ? 1 : 2; }
+__host__ __device__ constexpr int sentinel_region(int dense_tw) {
+    return dense_tw == 1024 ? 0 : dense_tw == 2048 ? 1 : dense_tw == 4096 ? 3 : 2;
+}
 
 // ---------------------------------------------------------------------------------------
 // Tile-major B in record groups.  Tiles are taken RG = 1 << rgs at a time (a record group:
