@@ -358,6 +358,38 @@ def _random_rows(rng, rows, cols, per_row):
     return M
 
 
+@pytest.mark.parametrize("ncols,choices", [(20000, [0, 40, 300, 700, 1500]), (140000, [0, 100, 300, 600, 900])])
+def test_symbolic_segments_long_and_ragged(ncols, choices):
+    """The segment symbolic kernel's round-6 loop (k_tile_sym_seg, SPG_SYM_PF): a round's first
+    three steps of column loads together, the next round's extents as raw words a round later,
+    then the extra steps of segments longer than 384 columns.  B rows of 0 to 1500 entries,
+    A rows whose entry counts are not multiples of 16, an empty A row; whole-row symbolic tiles
+    (20000 columns, dense 2048-column numeric tiles) and 65536-column symbolic tiles of a
+    140000-column B (three per row, the last ragged; sparse numeric tiles); bit-exact for every
+    algorithm."""
+    from spmm_amd import cusparse
+    from spmm_amd.sparse import csr_matrix
+    rng = np.random.default_rng(41)
+    k = 20000
+    lens = rng.choice(choices, size=k, p=[0.05, 0.25, 0.4, 0.2, 0.1])
+    r = np.repeat(np.arange(k), lens)
+    B = sp.csr_matrix((rng.standard_normal(r.size), (r, rng.integers(0, ncols, size=r.size))), shape=(k, ncols))
+    B.sum_duplicates()
+    B.sort_indices()
+    alen = rng.integers(1, 40, size=160)
+    alen[7] = 0
+    ra = np.repeat(np.arange(160), alen)
+    A = sp.csr_matrix((rng.standard_normal(ra.size), (ra, rng.integers(0, k, size=ra.size))), shape=(160, k))
+    A.sum_duplicates()
+    A.sort_indices()
+    dA, dB = csr_matrix(A, device=_dev()), csr_matrix(B, device=_dev())
+    info = cusparse.plan_info(dA, dB, alg=2)
+    assert info["path"] == "tile", info
+    ref = oracle.spgemm(A, B, keep_zeros=True, sort=True)
+    for alg, cf in [(1, 0.2), (2, 0.2), ("3c", 0.1)]:
+        _assert_same(_gpu(A, B, alg=alg, cf=cf), ref)
+
+
 def test_tile_path_cooperative_groups_with_padding():
     """Config 5's cooperative record groups on a shape whose tile count does not divide by 8:
     300000 columns -> 37 numeric tiles of 8192 (record groups of 8: the last holds 5 real tiles
