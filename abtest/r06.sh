@@ -45,6 +45,13 @@ for step in "$@"; do
         echo "== $v"; python3 profiles/summarize.py $P | grep -E "k_tile_dn" | tee $P/summary.txt
         find $P -name "*.csv" -delete
       done ;;
+    kt4)
+      for v in $arg; do
+        P=gpurun_out/r06/kt4_$v; mkdir -p $P
+        SPG_LIB=$PWD/spmm_amd/lib/libv_$v.so timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv -d $P -o kt -- python3 bench.py --no-config2 --no-alg3-chunked --cpu-seconds 0 --steps 2 --warmup 1 > $P/kt.log 2>&1 || { echo "kt4 $v failed"; tail -3 $P/kt.log; exit 1; }
+        echo "== $v"; python3 profiles/summarize.py $P | head -12 | tee $P/summary.txt
+        find $P -name "*.csv" -delete
+      done ;;
     f32)
       for sh in ${F32_SHAPES:-65536:0.005 16384:0.01 8192:0.01 8192:0.1}; do
         n=${sh%%:*}; d=${sh#*:}
